@@ -1,0 +1,96 @@
+"""ctypes binding of libgpfit.so (the C ABI declared in include/gpfit.h).
+
+This is the whole host/device boundary: every product computation goes through one of these
+symbols.  There is no CPU fallback — if the library is missing or cannot be loaded, every
+entry point raises :class:`GPFitUnavailable`.
+
+``torch`` is imported before the library is loaded on purpose: torch's bundled HIP runtime
+(soname ``libamdhip64.so.7``) is then the one libgpfit binds to, so torch tensors, streams and
+our kernels share one runtime and one device context.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+from ._build import LIB_PATH
+
+c_int, c_ll, c_void_p, c_double_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p
+
+GPFIT_ERR_HIP = -1000
+
+# name -> (restype, argtypes); pointers are passed as integers (tensor.data_ptr()).
+SIGNATURES = {
+    "gp_version": (c_int, []),
+    "gp_padded_n": (c_int, [c_int]),
+    "gp_gram_ardse": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                              c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p]),
+    "gp_cross_ardse": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                               c_void_p, c_int, c_void_p, c_void_p, c_int, c_ll, c_int,
+                               c_void_p]),
+    "gp_potrf_inv": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_ll, c_int,
+                             c_void_p, c_void_p, c_void_p]),
+    "gp_predict_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
+    "gp_predict": (c_int, [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_int, c_int,
+                           c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                           c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int, c_void_p]),
+    "gp_trmv": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
+                        c_void_p]),
+    "gp_nll": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                       c_void_p, c_int, c_void_p]),
+}
+
+
+class GPFitUnavailable(RuntimeError):
+    """libgpfit.so is not built or cannot be loaded (no fallback path exists)."""
+
+
+class GPFitError(RuntimeError):
+    """A libgpfit entry point returned a non-zero status."""
+
+    def __init__(self, func: str, rc: int):
+        if rc <= GPFIT_ERR_HIP:
+            msg = f"{func}: HIP error {GPFIT_ERR_HIP - rc}"
+        else:
+            msg = f"{func}: invalid argument #{-rc}"
+        super().__init__(msg)
+        self.func = func
+        self.rc = rc
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the configured library handle."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise GPFitUnavailable(
+            f"{LIB_PATH} is missing: build it with `python -m gladsgp_amd._build` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    try:
+        handle = ctypes.CDLL(LIB_PATH)
+    except OSError as exc:  # pragma: no cover - environment specific
+        raise GPFitUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = handle
+    return handle
+
+
+def call(name: str, *args) -> int:
+    """Invoke entry point ``name``; raise :class:`GPFitError` on a non-zero return."""
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise GPFitError(name, rc)
+    return rc
+
+
+def exported_symbols() -> list[str]:
+    return list(SIGNATURES)

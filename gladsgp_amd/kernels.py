@@ -1,0 +1,214 @@
+"""Tensor-level entry points over libgpfit (device memory and streams from PyTorch-ROCm).
+
+PyTorch is plumbing here: it owns the device buffers and the current HIP stream; every
+arithmetic step runs in the HIP kernels behind :mod:`gladsgp_amd._capi`.
+
+Layout convention: libgpfit is column-major (LAPACK).  A column-major n x n matrix M is held in
+a torch tensor ``buf`` of shape (batch, n_cols, ld) with ``buf[b, j, i] = M[i, j]``; the
+logical matrix is ``buf.transpose(-1, -2)``.  Symmetric matrices (the Gram) look the same
+either way.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _capi
+
+F64 = torch.float64
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _check_device(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP device tensor (got {t.device}); "
+                         "libgpfit has no CPU path")
+
+
+def _as_f64(x, device, name) -> torch.Tensor:
+    t = torch.as_tensor(x, dtype=F64, device=device)
+    _check_device(t, name)
+    return t.contiguous()
+
+
+def _per_batch(x, batch: int, device, name) -> torch.Tensor:
+    t = _as_f64(x, device, name).reshape(-1)
+    if t.numel() == 1 and batch > 1:
+        t = t.expand(batch).contiguous()
+    if t.numel() != batch:
+        raise ValueError(f"{name}: expected {batch} values, got {t.numel()}")
+    return t
+
+
+def _beta(beta, batch: int, d: int, device) -> torch.Tensor:
+    t = _as_f64(beta, device, "beta")
+    if t.dim() == 1:
+        t = t.reshape(1, -1)
+    if t.shape[0] == 1 and batch > 1:
+        t = t.expand(batch, t.shape[1]).contiguous()
+    if tuple(t.shape) != (batch, d):
+        raise ValueError(f"beta: expected shape ({batch}, {d}), got {tuple(t.shape)}")
+    return t
+
+
+def padded_n(n: int) -> int:
+    return _capi.lib().gp_padded_n(int(n))
+
+
+def gram(X: torch.Tensor, beta, s, delta, batch: int | None = None) -> torch.Tensor:
+    """G[b] = s[b] exp(-sum_k beta[b,k] (x_i - x_j)_k^2) + delta[b] I   -> (batch, n, n)."""
+    X = _as_f64(X, None if not torch.is_tensor(X) else X.device, "X")
+    n, d = X.shape
+    bt = torch.as_tensor(beta)
+    batch = batch or (bt.shape[0] if bt.dim() == 2 else 1)
+    dev = X.device
+    beta_t = _beta(beta, batch, d, dev)
+    s_t = _per_batch(s, batch, dev, "s")
+    d_t = _per_batch(delta, batch, dev, "delta")
+    G = torch.empty((batch, n, n), dtype=F64, device=dev)
+    _capi.call("gp_gram_ardse", X.data_ptr(), n, d, d, beta_t.data_ptr(), d, s_t.data_ptr(),
+               d_t.data_ptr(), G.data_ptr(), n, n * n, batch, _stream(dev))
+    return G
+
+
+def cross(X: torch.Tensor, Xs: torch.Tensor, beta, s, batch: int | None = None) -> torch.Tensor:
+    """K*^T[b] (n x m) held column-major: returns tensor (batch, m, n), [b, j, i] = K*[j, i]."""
+    X = _as_f64(X, X.device, "X")
+    Xs = _as_f64(Xs, X.device, "Xs")
+    n, d = X.shape
+    m = Xs.shape[0]
+    bt = torch.as_tensor(beta)
+    batch = batch or (bt.shape[0] if bt.dim() == 2 else 1)
+    beta_t = _beta(beta, batch, d, X.device)
+    s_t = _per_batch(s, batch, X.device, "s")
+    Kt = torch.empty((batch, m, n), dtype=F64, device=X.device)
+    _capi.call("gp_cross_ardse", X.data_ptr(), n, d, Xs.data_ptr(), m, d, d, beta_t.data_ptr(),
+               d, s_t.data_ptr(), Kt.data_ptr(), n, m * n, batch, _stream(X.device))
+    return Kt
+
+
+@dataclass
+class Cholesky:
+    """Result of :func:`cholesky_inverse` (buffers are column-major, see module doc)."""
+
+    n: int
+    a_buf: torch.Tensor      # (batch, n, n): lower triangle holds L (col-major)
+    linv_buf: torch.Tensor   # (batch, npad, npad): L^-1 (col-major, zero-padded)
+    info: torch.Tensor       # (batch,) int32, LAPACK potrf info
+    logdet: torch.Tensor     # (batch,) float64, log|A|
+
+    @property
+    def L(self) -> torch.Tensor:
+        return torch.tril(self.a_buf.transpose(-1, -2))
+
+    @property
+    def Linv(self) -> torch.Tensor:
+        return self.linv_buf.transpose(-1, -2)[:, : self.n, : self.n]
+
+    def check(self) -> None:
+        bad = torch.nonzero(self.info).flatten().tolist()
+        if bad:
+            raise ValueError(f"matrix not positive definite (info={self.info[bad].tolist()} for "
+                             f"problems {bad})")
+
+
+def cholesky_inverse(G: torch.Tensor, overwrite: bool = True) -> Cholesky:
+    """Blocked MFMA Cholesky A = L L^T with L^-1, logdet and LAPACK info per problem."""
+    _check_device(G, "G")
+    if G.dtype != F64:
+        raise TypeError("G must be float64")
+    if G.dim() == 2:
+        G = G.unsqueeze(0)
+    batch, n, n2 = G.shape
+    if n != n2:
+        raise ValueError("G must be square")
+    A = G if (overwrite and G.is_contiguous()) else G.contiguous().clone()
+    npad = padded_n(n)
+    Linv = torch.empty((batch, npad, npad), dtype=F64, device=G.device)
+    info = torch.empty(batch, dtype=torch.int32, device=G.device)
+    logdet = torch.empty(batch, dtype=F64, device=G.device)
+    _capi.call("gp_potrf_inv", A.data_ptr(), n, n, n * n, Linv.data_ptr(), npad, npad * npad,
+               batch, info.data_ptr(), logdet.data_ptr(), _stream(G.device))
+    return Cholesky(n, A, Linv, info, logdet)
+
+
+class PredictWorkspace:
+    """Reusable device scratch for :func:`predict` (grown on demand, never shrunk)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        return self.buf
+
+
+_DEFAULT_WS = PredictWorkspace()
+
+
+def predict(chol: Cholesky, X: torch.Tensor, Xs: torch.Tensor, beta, s, s_pred, w,
+            m_chunk: int = 0, workspace: PredictWorkspace | None = None,
+            out: tuple[torch.Tensor, torch.Tensor] | None = None):
+    """Posterior mean / marginal variance at Xs for every problem: returns (batch, m) x 2."""
+    dev = chol.linv_buf.device
+    X = _as_f64(X, dev, "X")
+    Xs = _as_f64(Xs, dev, "Xs")
+    n, d = X.shape
+    if n != chol.n:
+        raise ValueError("X rows do not match the factorisation")
+    m = Xs.shape[0]
+    batch = chol.linv_buf.shape[0]
+    npad = chol.linv_buf.shape[1]
+    beta_t = _beta(beta, batch, d, dev)
+    s_t = _per_batch(s, batch, dev, "s")
+    sp_t = _per_batch(s_pred, batch, dev, "s_pred")
+    w_t = _as_f64(w, dev, "w")
+    if w_t.dim() == 1:
+        w_t = w_t.reshape(1, -1)
+    if tuple(w_t.shape) != (batch, n):
+        raise ValueError(f"w: expected shape ({batch}, {n}), got {tuple(w_t.shape)}")
+    if out is None:
+        mean = torch.empty((batch, m), dtype=F64, device=dev)
+        var = torch.empty((batch, m), dtype=F64, device=dev)
+    else:
+        mean, var = out
+    nbytes = _capi.lib().gp_predict_ws_bytes(n, m, batch, int(m_chunk))
+    ws = (workspace or _DEFAULT_WS).get(nbytes, dev)
+    _capi.call("gp_predict", chol.linv_buf.data_ptr(), npad, npad * npad, X.data_ptr(), d,
+               Xs.data_ptr(), d, n, m, d, beta_t.data_ptr(), d, s_t.data_ptr(),
+               sp_t.data_ptr(), w_t.data_ptr(), n, mean.data_ptr(), var.data_ptr(),
+               mean.stride(0) if batch > 1 else m, batch, ws.data_ptr(), ws.numel(),
+               int(m_chunk), _stream(dev))
+    return mean, var
+
+
+def nll(chol: Cholesky, w) -> torch.Tensor:
+    """1/2 ||L^-1 w||^2 + 1/2 log|A| per problem (GPmodule objective, no 2pi)."""
+    dev = chol.linv_buf.device
+    batch = chol.linv_buf.shape[0]
+    npad = chol.linv_buf.shape[1]
+    n = chol.n
+    w_t = _as_f64(w, dev, "w").reshape(batch, n)
+    out = torch.empty(batch, dtype=F64, device=dev)
+    work = torch.empty((batch, n), dtype=F64, device=dev)
+    _capi.call("gp_nll", chol.linv_buf.data_ptr(), npad, npad * npad, n, w_t.data_ptr(), n,
+               chol.logdet.data_ptr(), out.data_ptr(), work.data_ptr(), batch, _stream(dev))
+    return out
+
+
+def trmv(chol: Cholesky, w) -> torch.Tensor:
+    """z = L^-1 w per problem -> (batch, n)."""
+    dev = chol.linv_buf.device
+    batch = chol.linv_buf.shape[0]
+    npad = chol.linv_buf.shape[1]
+    n = chol.n
+    w_t = _as_f64(w, dev, "w").reshape(batch, n)
+    z = torch.empty((batch, n), dtype=F64, device=dev)
+    _capi.call("gp_trmv", chol.linv_buf.data_ptr(), npad, npad * npad, n, w_t.data_ptr(), n,
+               z.data_ptr(), n, batch, _stream(dev))
+    return z

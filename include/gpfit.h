@@ -1,0 +1,123 @@
+/*
+ * libgpfit — MI355X (gfx950) fp64 Gaussian-process fit/predict kernels behind a C ABI.
+ *
+ * Drop-in boundary for timghill/GladsGP's GP hot path.  The reference is pure Python: its GP
+ * arithmetic lives in the un-vendored SEPIA fork (requirements-cc.txt:55) and GPmodule
+ * (requirements-cc.txt:20), called from src/model.py and the analysis drivers.  There is no FFI
+ * in the reference, so each entry point below names the reference call it replaces; the
+ * Python-side binding is gladsgp_amd/_capi.py (ctypes) and is shown in INTEGRATION.md.
+ *
+ * Conventions (all entry points):
+ *  - every pointer is caller-owned DEVICE memory (the library never allocates; the predict
+ *    workspace is sized by gp_predict_ws_bytes() and passed in);
+ *  - matrices are column-major with a leading dimension (LAPACK layout), element (i,j) at
+ *    A[i + j*ld]; design matrices X (n x d) are row-major with row stride ldx >= d;
+ *  - `batch` independent problems share X / Xs; per-problem operands advance by the given
+ *    stride (matrices), by ldbeta (beta rows), by 1 (s, delta, s_pred, info, logdet) and by
+ *    ldw / ldo (w_hat, mean, var columns);
+ *  - stream-ordered and asynchronous on `stream`; no host synchronisation, so calls can be
+ *    captured into a hipGraph;
+ *  - return 0 on success, -k when argument k is invalid (LAPACK style), or
+ *    GPFIT_ERR_HIP - hipError_t for a launch failure.  A non-positive-definite pivot is not an
+ *    error return: it is reported per problem in info[b] (LAPACK potrf semantics).
+ */
+#ifndef GPFIT_H
+#define GPFIT_H
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPFIT_ERR_HIP (-1000)
+#define GPFIT_MAX_DIM 32      /* largest input dimension d supported by the kernels      */
+#define GPFIT_TILE 128        /* row padding of the L^-1 buffer (predict MFMA tile edge) */
+
+/* Library version (major*10000 + minor*100 + patch). */
+int gp_version(void);
+
+/* Rows/columns of the L^-1 buffer gp_potrf_inv fills: n rounded up to GPFIT_TILE. */
+int gp_padded_n(int n);
+
+/*
+ * ARD squared-exponential Gram with jitter, per problem b:
+ *   G_b[i + j*ldg] = s[b] * exp(-sum_k beta_b[k] (X[i,k] - X[j,k])^2) + delta[b] * (i == j)
+ * Replaces SEPIA SepiaDistCov.compute_cov_mat(beta, lamz, lams) (s = 1/lamUz,
+ * delta = 1/lamWs + 1/(lamWOs*LamSim)) as used by SepiaModel.logLik and
+ * SepiaEmulatorPrediction (src/model.py:106, analysis/time_predictions.py:76), the explicit
+ * Gram of examples/01_Gaussian_random_fields.ipynb:135-141 and GPmodule's
+ * squared_exponential (examples/02_univariate_GP_regression.ipynb:80).
+ */
+int gp_gram_ardse(const double* X, int n, int d, int ldx,
+                  const double* beta, int ldbeta, const double* s, const double* delta,
+                  double* G, int ldg, long long strideG, int batch, hipStream_t stream);
+
+/*
+ * Cross-covariance, transposed so each test point's column is contiguous:
+ *   Kt_b[i + j*ldk] = s[b] * exp(-sum_k beta_b[k] (X[i,k] - Xs[j,k])^2),  i < n, j < m.
+ * Replaces the Kvec / SigWWb cross-covariance of SepiaEmulatorPrediction and
+ * examples/02...ipynb:226.
+ */
+int gp_cross_ardse(const double* X, int n, int ldx, const double* Xs, int m, int ldxs, int d,
+                   const double* beta, int ldbeta, const double* s,
+                   double* Kt, int ldk, long long strideK, int batch, hipStream_t stream);
+
+/*
+ * Blocked Cholesky with simultaneous triangular inverse, per problem b:
+ *   A_b = L_b L_b^T (L_b overwrites the lower triangle of A_b; the strict upper triangle is
+ *   left untouched, as LAPACK dpotrf('L')), Linv_b = L_b^-1 (lower; the upper triangle and the
+ *   padding rows/cols n..gp_padded_n(n)-1 are zeroed), logdet[b] = log|A_b| = 2 sum log L_ii,
+ *   info[b] = 0, or j (1-based) when the leading minor of order j is not positive definite
+ *   (then L_b / Linv_b / logdet[b] are unspecified).
+ * Linv_b needs ldinv >= gp_padded_n(n) and gp_padded_n(n) columns.  info / logdet may be NULL.
+ * Replaces the dense SPD factorisation / solve inside SEPIA's likelihood and prediction
+ * (LAPACK potrf/gesv), scipy.linalg.cholesky in examples/01...ipynb:66,144 and GPmodule's
+ * K_inv (examples/02...ipynb:232).
+ */
+int gp_potrf_inv(double* A, int n, int lda, long long strideA,
+                 double* Linv, int ldinv, long long strideInv,
+                 int batch, int* info, double* logdet, hipStream_t stream);
+
+/* Bytes of device workspace gp_predict needs for (n, m, batch) with test-point chunk m_chunk
+ * (0 = library default).  Workspace contents are scratch (no state between calls).         */
+long long gp_predict_ws_bytes(int n, int m, int batch, int m_chunk);
+
+/*
+ * Posterior mean and marginal variance of `batch` GPs at m test points:
+ *   z_b = Linv_b w_b,  V = Linv_b Kt_b (never stored),
+ *   mean_b[j] = sum_i V[i,j] z_b[i]          = k*_j^T A_b^-1 w_b
+ *   var_b[j]  = s_pred[b] - sum_i V[i,j]^2   = s_pred[b] - k*_j^T A_b^-1 k*_j
+ * with w_b = w_hat + b*ldw (n values), mean_b = mean + b*ldo, var_b = var + b*ldo (m values).
+ * Linv comes from gp_potrf_inv with the same X, beta, s.  Replaces SepiaEmulatorPrediction's
+ * predictive mean / covariance diagonal (analysis/time_predictions.py:76-78,
+ * assess_all_models.py:489, sensitivity_indices.py:85) and examples/02...ipynb:232-233.
+ */
+int gp_predict(const double* Linv, int ldinv, long long strideInv,
+               const double* X, int ldx, const double* Xs, int ldxs, int n, int m, int d,
+               const double* beta, int ldbeta, const double* s, const double* s_pred,
+               const double* w_hat, int ldw, double* mean, double* var, int ldo,
+               int batch, void* ws, long long ws_bytes, int m_chunk, hipStream_t stream);
+
+/*
+ * z_b = Linv_b w_b (lower-triangular gemv, n rows), z_b = z + b*ldz.
+ * Building block of the likelihood (quadratic form w^T A^-1 w = ||z||^2).
+ */
+int gp_trmv(const double* Linv, int ldinv, long long strideInv, int n,
+            const double* w, int ldw, double* z, int ldz, int batch, hipStream_t stream);
+
+/*
+ * GP negative log-likelihood per problem:  nll[b] = 1/2 ||Linv_b w_b||^2 + 1/2 logdet[b]
+ * (no 2*pi term), with Linv / logdet from gp_potrf_inv; `work` holds batch*n doubles.
+ * Replaces GPmodule's MLE objective (examples/02_univariate_GP_regression.ipynb:80-83, known
+ * answer fun = -3.989954265337257 at :70-72) and the per-PC Gaussian term of SEPIA's logLik
+ * evaluated by SepiaModel.do_mcmc (src/model.py:234-235).
+ */
+int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
+           const double* w, int ldw, const double* logdet, double* nll, double* work,
+           int batch, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPFIT_H */

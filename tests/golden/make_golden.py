@@ -1,0 +1,128 @@
+"""Regenerate the committed golden fixtures (run in the build container, NOT on the GPU box).
+
+    python tests/golden/make_golden.py [--reference /root/reference]
+
+Writes only data (.npz / .json / .csv) into tests/golden/:
+
+* ``synthetic_{train,test}_standard.csv`` — the reference's own design fixtures (512x8 and
+  100x8, ``experiments/synthetic/expdesign/``; identical copies in
+  ``examples/data/GlaDS_example/``), copied verbatim as data.
+* ``nb02_known_answer.json`` — the MLE optimum printed by
+  ``examples/02_univariate_GP_regression.ipynb`` (cell output at :70-72 of the raw JSON), the
+  notebook inputs (:43), and the oracle's restatement of that fit (BFGS from [1, 0.5]) plus
+  its 51-point posterior mean / sd at the optimum.
+* ``svd_ref_64x500.npz`` — outputs of the reference's own ``src/svd.py`` ``randomized_svd``
+  imported from the read-only reference tree, on a seeded float32 matrix with
+  ``np.random.seed(123)`` (p=8, k=None, q=1) and (p=25, k=0, q=1), together with the Gaussian
+  test matrices it drew, so the oracle restatement can be checked exactly.
+* ``c2_golden.npz`` — oracle GP outputs on the real 512x8 design (C2 recipe) at
+  256 test points: Gram spot values, logdet, mean, var, nll.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import gp_ref  # noqa: E402
+
+
+def copy_designs(ref: str) -> None:
+    src = os.path.join(ref, "experiments", "synthetic", "expdesign")
+    for name in ("synthetic_train_standard.csv", "synthetic_test_standard.csv"):
+        shutil.copyfile(os.path.join(src, name), os.path.join(HERE, name))
+
+
+def notebook_known_answer(ref: str) -> None:
+    nb = json.load(open(os.path.join(ref, "examples", "02_univariate_GP_regression.ipynb")))
+    printed = None
+    for cell in nb["cells"]:
+        for out in cell.get("outputs", []):
+            text = "".join(out.get("text", []))
+            if "fun:" in text and "nit:" in text:
+                printed = text
+    assert printed is not None, "notebook output not found"
+    fun = float(printed.split("fun:")[1].split()[0])
+    xs = printed.split("x: [")[1].split("]")[0].split()
+    nit = int(printed.split("nit:")[1].split()[0])
+    x = np.linspace(1 / 8, 7 / 8, 5).reshape(-1, 1)
+    y = x * np.sin(2 * np.pi * x)
+    res = gp_ref.fit_gpmodule(x, y, x0=(1.0, 0.5), nugget=1e-3)
+    theta = np.abs(res.x)
+    s, beta, delta = gp_ref.gpmodule_theta_to_kernel(theta, 1e-3)
+    xpred = np.linspace(0, 1, 51).reshape(-1, 1)
+    mean, var = gp_ref.predict(x, xpred, y.ravel(), beta, s, delta, s_pred=s)
+    out = {
+        "source": "examples/02_univariate_GP_regression.ipynb (printed scipy result)",
+        "printed_fun": fun, "printed_x": [float(v) for v in xs], "printed_nit": nit,
+        "x_train": x.ravel().tolist(), "y_train": y.ravel().tolist(),
+        "x_pred": xpred.ravel().tolist(), "nugget": 1e-3,
+        "oracle_fun": float(res.fun), "oracle_theta": theta.tolist(),
+        "oracle_mean": mean.tolist(), "oracle_var": var.tolist(),
+    }
+    json.dump(out, open(os.path.join(HERE, "nb02_known_answer.json"), "w"), indent=1)
+    print("nb02: printed", fun, xs, "oracle", res.fun, theta)
+
+
+def svd_reference(ref: str) -> None:
+    spec = importlib.util.spec_from_file_location("ref_svd", os.path.join(ref, "src", "svd.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rng = np.random.default_rng(7)
+    base = rng.standard_normal((64, 12)) @ rng.standard_normal((12, 500))
+    X = (base + 0.05 * rng.standard_normal((64, 500))).astype(np.float32)
+    out = {"X": X}
+    for tag, (p, k) in {"p8": (8, None), "p25k0": (25, 0)}.items():
+        np.random.seed(123)
+        U, S, Vh = mod.randomized_svd(X, p, k=k, q=1)
+        np.random.seed(123)
+        kk = p if k is None else k
+        omega = np.random.normal(size=(X.shape[1], p + kk)).astype(np.float32)
+        out.update({f"{tag}_U": U, f"{tag}_S": S, f"{tag}_Vh": Vh, f"{tag}_omega": omega})
+    np.savez_compressed(os.path.join(HERE, "svd_ref_64x500.npz"), **out)
+    print("svd golden written")
+
+
+def c2_golden() -> None:
+    X = np.loadtxt(os.path.join(HERE, "synthetic_train_standard.csv"), delimiter=",",
+                   skiprows=1, comments=None)
+    a = np.random.default_rng(1).uniform(0, 1, 8)
+    y = np.sin(2 * np.pi * X @ a) + 0.1 * np.sum(X * X, axis=1)
+    beta = np.random.default_rng(3).uniform(0.5, 5.0, 8)
+    Xs = np.random.default_rng(2).random((256, 8))
+    s, delta = 1.0, 1e-6
+    G = gp_ref.gram_ardse(X, beta, s, delta)
+    L, info = gp_ref.cholesky(G)
+    logdet = 2 * np.sum(np.log(np.diag(L)))
+    mean, var = gp_ref.predict(X, Xs, y, beta, s, delta)
+    import scipy.linalg as sla
+    z = sla.solve_triangular(L, y, lower=True)
+    nll = 0.5 * z @ z + 0.5 * logdet
+    idx = np.random.default_rng(5).integers(0, 512, size=(64, 2))
+    np.savez_compressed(os.path.join(HERE, "c2_golden.npz"), X=X, y=y, beta=beta, Xs=Xs,
+                        s=s, delta=delta, gram_idx=idx, gram_vals=G[idx[:, 0], idx[:, 1]],
+                        logdet=logdet, mean=mean, var=var, nll=nll)
+    print("c2 golden: logdet", logdet, "nll", nll)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    args = ap.parse_args()
+    copy_designs(args.reference)
+    notebook_known_answer(args.reference)
+    svd_reference(args.reference)
+    c2_golden()
+
+
+if __name__ == "__main__":
+    main()

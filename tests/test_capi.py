@@ -1,0 +1,90 @@
+"""CPU: the C-ABI library builds, loads, and exports every symbol include/gpfit.h declares.
+
+No device work happens here: only host-side entry points (sizes, argument validation that
+returns before any launch) are called.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gpfit.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gp_[a-z_0-9]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gladsgp_amd import _build, _capi
+    _build.build_library()
+    return _capi.lib()
+
+
+def test_header_declares_expected_entry_points():
+    names = _declared()
+    for must in ("gp_gram_ardse", "gp_cross_ardse", "gp_potrf_inv", "gp_predict",
+                 "gp_predict_ws_bytes", "gp_nll", "gp_trmv", "gp_padded_n", "gp_version"):
+        assert must in names
+
+
+def test_every_declared_symbol_is_exported(lib):
+    from gladsgp_amd import _build, _capi
+    out = subprocess.run(["nm", "-D", "--defined-only", _build.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gp_[a-z_0-9]+)", out))
+    for name in _declared():
+        assert name in exported, name
+        assert name in _capi.SIGNATURES, f"{name} lacks a ctypes signature"
+
+
+def test_library_has_gfx950_code_object():
+    from gladsgp_amd import _build
+    data = open(_build.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_host_side_helpers(lib):
+    assert lib.gp_version() >= 100
+    assert lib.gp_padded_n(1) == 128
+    assert lib.gp_padded_n(4096) == 4096
+    assert lib.gp_padded_n(4097) == 4224
+    assert lib.gp_padded_n(0) == 0
+    ws = lib.gp_predict_ws_bytes(4096, 100000, 1, 0)
+    assert ws > 4096 * 4096 * 8 // 4
+    # a given chunk bounds the cross-covariance scratch
+    small = lib.gp_predict_ws_bytes(4096, 100000, 1, 1024)
+    assert small < ws
+    assert lib.gp_predict_ws_bytes(0, 10, 1, 0) == 0
+
+
+def test_argument_validation_returns_lapack_style_codes(lib):
+    # invalid arguments are rejected on the host before any launch
+    rc = lib.gp_gram_ardse(None, 10, 2, 2, None, 2, None, None, None, 10, 100, 1, None)
+    assert rc == -1
+    dummy = ctypes.c_void_p(16)
+    rc = lib.gp_gram_ardse(dummy, 10, 0, 2, dummy, 2, dummy, dummy, dummy, 10, 100, 1, None)
+    assert rc == -3   # d out of range
+    rc = lib.gp_gram_ardse(dummy, 10, 2, 2, dummy, 2, dummy, dummy, dummy, 5, 100, 1, None)
+    assert rc == -10  # ldg < n
+    rc = lib.gp_potrf_inv(dummy, 100, 100, 10000, dummy, 64, 4096, 1, None, None, None)
+    assert rc == -6   # ldinv < gp_padded_n(n)
+    rc = lib.gp_predict(dummy, 128, 128 * 128, dummy, 2, dummy, 2, 100, 10, 2, dummy, 2, dummy,
+                        dummy, dummy, 100, dummy, dummy, 10, 1, dummy, 0, 0, None)
+    assert rc == -22  # workspace too small
+    # zero-sized problems are a no-op
+    assert lib.gp_potrf_inv(dummy, 0, 1, 0, dummy, 1, 0, 1, None, None, None) == 0
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    from gladsgp_amd import _capi
+    monkeypatch.setattr(_capi, "_LIB", None)
+    monkeypatch.setattr(_capi, "LIB_PATH", str(tmp_path / "missing.so"))
+    with pytest.raises(_capi.GPFitUnavailable):
+        _capi.lib()

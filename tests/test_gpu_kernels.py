@@ -1,0 +1,243 @@
+"""GPU parity: libgpfit kernels vs the numpy fp64 oracle (called through the C ABI).
+
+Tolerances (fp64, stated per SURVEY §8c and measured):
+  Gram          max|dG| <= 8 eps * s          (exp differs by a few ulp between libm and ocml)
+  Cholesky      ||L L^T - G||_F / ||G||_F <= 1e-13 ; ||L^-1 L - I||_max <= 1e-9 (kappa-limited)
+  logdet        |d| <= 1e-9 * n
+  predict (C2)  max|dmean| <= 1e-8 max|mean| , max|dvar| <= 1e-9 s   (kappa(G) ~ 1e8 at 1e-6 jitter)
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gp_ref
+
+pytestmark = pytest.mark.gpu
+
+EPS = np.finfo(np.float64).eps
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from gladsgp_amd import kernels  # noqa: F401 (loads libgpfit.so)
+    return torch.device("cuda:0")
+
+
+def _t(x, dev):
+    return torch.as_tensor(np.asarray(x, dtype=np.float64), device=dev)
+
+
+def _c2(golden_dir):
+    return np.load(os.path.join(golden_dir, "c2_golden.npz"))
+
+
+def test_library_is_native(dev):
+    from gladsgp_amd import _capi
+    lib = _capi.lib()
+    assert lib.gp_version() >= 100
+    with open("/proc/self/maps") as f:
+        assert "libgpfit.so" in f.read()
+
+
+@pytest.mark.parametrize("n,d", [(1, 1), (7, 3), (64, 8), (129, 8), (512, 8), (300, 17)])
+def test_gram_matches_oracle(dev, n, d):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(n + d)
+    X = rng.random((n, d))
+    beta = rng.uniform(0.5, 5.0, d)
+    s, delta = 1.3, 1e-6
+    G = kernels.gram(_t(X, dev), _t(beta, dev), s, delta)[0].cpu().numpy()
+    ref = gp_ref.gram_ardse(X, beta, s, delta)
+    assert np.max(np.abs(G - ref)) <= 8 * EPS * s
+    np.testing.assert_array_equal(G, G.T)
+
+
+def test_gram_batched_and_c2_golden(dev, golden_dir):
+    from gladsgp_amd import kernels
+    g = _c2(golden_dir)
+    rng = np.random.default_rng(3)
+    betas = np.stack([g["beta"], rng.uniform(0.5, 5, 8), rng.uniform(0.1, 2, 8)])
+    s = np.array([1.0, 0.7, 2.0])
+    delta = np.array([1e-6, 1e-4, 1e-2])
+    G = kernels.gram(_t(g["X"], dev), _t(betas, dev), _t(s, dev), _t(delta, dev)).cpu().numpy()
+    idx = g["gram_idx"]
+    np.testing.assert_allclose(G[0][idx[:, 0], idx[:, 1]], g["gram_vals"], rtol=0, atol=8 * EPS)
+    for b in range(3):
+        ref = gp_ref.gram_ardse(g["X"], betas[b], s[b], delta[b])
+        assert np.max(np.abs(G[b] - ref)) <= 8 * EPS * s[b]
+
+
+def test_cross_matches_oracle(dev):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(11)
+    X, Xs = rng.random((200, 8)), rng.random((333, 8))
+    beta = rng.uniform(0.5, 5, 8)
+    Kt = kernels.cross(_t(X, dev), _t(Xs, dev), _t(beta, dev), 0.9)[0].cpu().numpy()
+    ref = gp_ref.cross_ardse(Xs, X, beta, 0.9)
+    assert np.max(np.abs(Kt - ref)) <= 8 * EPS
+
+
+@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 127, 128, 129, 200, 512, 1000])
+def test_cholesky_inverse(dev, n):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(n)
+    X = rng.random((n, 8))
+    beta = rng.uniform(0.5, 5, 8)
+    G = gp_ref.gram_ardse(X, beta, 1.0, 1e-4)
+    Gt = _t(G, dev).unsqueeze(0).contiguous()
+    ch = kernels.cholesky_inverse(Gt)
+    assert int(ch.info[0]) == 0
+    L = ch.L[0].cpu().numpy()
+    Linv = ch.Linv[0].cpu().numpy()
+    Lref = np.linalg.cholesky(G)
+    assert np.linalg.norm(L @ L.T - G) / np.linalg.norm(G) <= 1e-13
+    assert np.max(np.abs(L - Lref)) <= 1e-10 * np.max(np.abs(Lref))
+    assert np.max(np.abs(Linv @ L - np.eye(n))) <= 1e-9
+    np.testing.assert_allclose(float(ch.logdet[0]), 2 * np.sum(np.log(np.diag(Lref))),
+                               rtol=0, atol=1e-9 * n)
+    # padding of the L^-1 buffer and its upper triangle are zero
+    full = ch.linv_buf[0].transpose(0, 1).cpu().numpy()
+    assert np.all(np.triu(full, 1) == 0)
+    assert np.all(full[n:, :] == 0) and np.all(full[:, n:] == 0)
+
+
+def test_cholesky_upper_triangle_untouched(dev):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(2)
+    n = 150
+    X = rng.random((n, 4))
+    G = gp_ref.gram_ardse(X, np.ones(4), 1.0, 1e-3)
+    A = G.copy()
+    A[np.triu_indices(n, 1)] = 123.0   # LAPACK potrf('L') never reads/writes the upper part
+    At = _t(A.T.copy(), dev).unsqueeze(0).contiguous()   # column-major buffer
+    ch = kernels.cholesky_inverse(At)
+    buf = ch.a_buf[0].transpose(0, 1).cpu().numpy()
+    assert np.all(buf[np.triu_indices(n, 1)] == 123.0)
+    np.testing.assert_allclose(np.tril(buf), np.linalg.cholesky(G), atol=1e-12)
+
+
+@pytest.mark.parametrize("n,bad", [(10, 3), (100, 1), (100, 64), (100, 65), (300, 200)])
+def test_cholesky_info_not_pd(dev, n, bad):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(n)
+    A = rng.standard_normal((n, n))
+    G = A @ A.T + n * np.eye(n)
+    G[bad - 1, bad - 1] = -1.0
+    _, info_ref = gp_ref.cholesky(G)
+    ch = kernels.cholesky_inverse(_t(G, dev).unsqueeze(0).contiguous())
+    assert int(ch.info[0]) == info_ref == bad
+
+
+def test_cholesky_batch_mixed_info(dev):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(9)
+    n = 96
+    Gs = []
+    for b in range(4):
+        A = rng.standard_normal((n, n))
+        G = A @ A.T + n * np.eye(n)
+        if b == 2:
+            G[70, 70] = -3.0
+        Gs.append(G)
+    ch = kernels.cholesky_inverse(_t(np.stack(Gs), dev).contiguous())
+    assert ch.info.cpu().tolist() == [0, 0, 71, 0]
+    for b in (0, 1, 3):
+        L = ch.L[b].cpu().numpy()
+        assert np.linalg.norm(L @ L.T - Gs[b]) / np.linalg.norm(Gs[b]) <= 1e-13
+
+
+def _predict_gpu(dev, X, Xs, w, beta, s, delta, s_pred=None, m_chunk=0):
+    from gladsgp_amd import kernels
+    s_pred = s if s_pred is None else s_pred
+    G = kernels.gram(_t(X, dev), _t(beta, dev), s, delta)
+    ch = kernels.cholesky_inverse(G)
+    ch.check()
+    mean, var = kernels.predict(ch, _t(X, dev), _t(Xs, dev), _t(beta, dev), s, s_pred,
+                                _t(w, dev), m_chunk=m_chunk)
+    return mean[0].cpu().numpy(), var[0].cpu().numpy()
+
+
+def test_predict_c2_golden(dev, golden_dir):
+    g = _c2(golden_dir)
+    mean, var = _predict_gpu(dev, g["X"], g["Xs"], g["y"], g["beta"], float(g["s"]),
+                             float(g["delta"]))
+    assert np.max(np.abs(mean - g["mean"])) <= 1e-8 * np.max(np.abs(g["mean"]))
+    assert np.max(np.abs(var - g["var"])) <= 1e-9 * float(g["s"])
+
+
+def test_predict_c2_full_m10k(dev, golden_dir):
+    """BASELINE config 2: real 512x8 design, m = 10k seeded test points."""
+    g = _c2(golden_dir)
+    Xs = np.random.default_rng(2).random((10000, 8))
+    mean_ref, var_ref = gp_ref.predict(g["X"], Xs, g["y"], g["beta"], 1.0, 1e-6)
+    mean, var = _predict_gpu(dev, g["X"], Xs, g["y"], g["beta"], 1.0, 1e-6)
+    assert np.max(np.abs(mean - mean_ref)) <= 1e-8 * np.max(np.abs(mean_ref))
+    assert np.max(np.abs(var - var_ref)) <= 1e-9
+
+
+@pytest.mark.parametrize("n,m,d,chunk", [(1, 1, 1, 0), (5, 51, 1, 0), (65, 129, 3, 0),
+                                         (130, 300, 8, 128), (256, 1000, 8, 384),
+                                         (700, 257, 16, 0)])
+def test_predict_edges(dev, n, m, d, chunk):
+    rng = np.random.default_rng(n * 7 + m)
+    X, Xs = rng.random((n, d)), rng.random((m, d))
+    beta = rng.uniform(0.5, 3, d)
+    w = rng.standard_normal(n)
+    s, delta = 1.5, 1e-3
+    mean_ref, var_ref = gp_ref.predict(X, Xs, w, beta, s, delta, s_pred=s + 0.01)
+    mean, var = _predict_gpu(dev, X, Xs, w, beta, s, delta, s_pred=s + 0.01, m_chunk=chunk)
+    np.testing.assert_allclose(mean, mean_ref, rtol=0, atol=1e-9 * max(1, np.abs(mean_ref).max()))
+    np.testing.assert_allclose(var, var_ref, rtol=0, atol=1e-10 * s)
+
+
+def test_predict_batched_per_problem_params(dev):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(4)
+    n, m, d, B = 300, 500, 8, 5
+    X, Xs = rng.random((n, d)), rng.random((m, d))
+    betas = rng.uniform(0.5, 4, (B, d))
+    s = rng.uniform(0.5, 2, B)
+    delta = rng.uniform(1e-5, 1e-2, B)
+    sp = s + rng.uniform(0, 0.1, B)
+    W = rng.standard_normal((B, n))
+    G = kernels.gram(_t(X, dev), _t(betas, dev), _t(s, dev), _t(delta, dev))
+    ch = kernels.cholesky_inverse(G)
+    mean, var = kernels.predict(ch, _t(X, dev), _t(Xs, dev), _t(betas, dev), _t(s, dev),
+                                _t(sp, dev), _t(W, dev), m_chunk=256)
+    mean, var = mean.cpu().numpy(), var.cpu().numpy()
+    for b in range(B):
+        mr, vr = gp_ref.predict(X, Xs, W[b], betas[b], s[b], delta[b], s_pred=sp[b])
+        np.testing.assert_allclose(mean[b], mr, atol=1e-9 * np.abs(mr).max())
+        np.testing.assert_allclose(var[b], vr, atol=1e-10)
+
+
+def test_nll_known_answer(dev, golden_dir):
+    """GPmodule objective at the notebook-02 optimum (fun = -3.989954265337257)."""
+    from gladsgp_amd import kernels
+    ka = json.load(open(os.path.join(golden_dir, "nb02_known_answer.json")))
+    x = np.asarray(ka["x_train"]).reshape(-1, 1)
+    y = np.asarray(ka["y_train"])
+    s, beta, delta = gp_ref.gpmodule_theta_to_kernel(ka["oracle_theta"], ka["nugget"])
+    ch = kernels.cholesky_inverse(kernels.gram(_t(x, dev), _t(beta, dev), s, delta))
+    v = float(kernels.nll(ch, _t(y, dev))[0])
+    assert abs(v - ka["oracle_fun"]) < 1e-12
+    assert abs(v - ka["printed_fun"]) < 1e-7
+
+
+def test_nll_c2(dev, golden_dir):
+    from gladsgp_amd import kernels
+    g = _c2(golden_dir)
+    ch = kernels.cholesky_inverse(kernels.gram(_t(g["X"], dev), _t(g["beta"], dev), 1.0, 1e-6))
+    assert abs(float(ch.logdet[0]) - float(g["logdet"])) <= 1e-8 * abs(float(g["logdet"]))
+    v = float(kernels.nll(ch, _t(g["y"], dev))[0])
+    assert abs(v - float(g["nll"])) <= 1e-8 * abs(float(g["nll"]))
+
+
+def test_cpu_tensor_rejected(dev):
+    from gladsgp_amd import kernels
+    with pytest.raises(ValueError):
+        kernels.gram(torch.zeros(4, 2, dtype=torch.float64), [1.0, 1.0], 1.0, 0.0)
