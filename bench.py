@@ -1,0 +1,224 @@
+#!/usr/bin/env python
+"""bench.py — GP posterior predictions/sec, fp64, C3 (n=4096 train, m=100k test, d=8).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one full pass of the hot path for one GP on one GPU, from hyperparameters to
+answers: ARD-SE Gram (n x n) -> blocked MFMA Cholesky + L^-1 -> fused cross-covariance /
+TRMM / mean+variance over that rank's m = 100k test points.  Inputs are HBM-resident before
+the timed region.  Ranks are independent test-point shards of one trained GP (weak scaling:
+every rank predicts its own 100k points; no collective inside a step), so
+value = N * 100k * K / max-over-ranks(time).
+
+rank 0 prints ONE JSON line with the metric, a roofline object for the dominant kernel
+(trmm_reduce, timed live with HIP events on its own stream via gp_profile_*), auxiliary
+rooflines, and a CPU baseline (the numpy fp64 oracle on the host cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+_CPU_THREADS = min(16, os.cpu_count() or 1)
+for _v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS"):
+    os.environ.setdefault(_v, str(_CPU_THREADS))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from gladsgp_amd import _capi, dist as gdist, kernels  # noqa: E402
+
+METRIC = "GP posterior predictions/sec fp64, n=4096 m=100k d=8; 1→8 GPU scaling"
+FP64_MFMA_PEAK_TFLOPS = 78.6    # MI355X dense FP64 matrix (spec); 70.1 measured (tools/probe_f64)
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E (spec); ~6300 achievable
+
+
+def c3_inputs(rank: int, n: int, m: int, d: int):
+    """SURVEY §8d C3 recipe (seeded).  Rank r predicts rows [r m, (r+1) m) of rng(2)'s stream."""
+    X = np.random.default_rng(0).random((n, d))
+    a = np.random.default_rng(1).uniform(0, 1, d)
+    y = np.sin(2 * np.pi * X @ a) + 0.1 * np.sum(X * X, axis=1)
+    beta = np.random.default_rng(3).uniform(0.5, 5.0, d)
+    Xs = np.random.default_rng(2).random(((rank + 1) * m, d))[rank * m:]
+    return X, y, beta, Xs, 1.0, 1e-6
+
+
+def cpu_baseline(X, y, beta, Xs, s, delta, budget_s: float):
+    """numpy fp64 oracle (Gram -> cholesky -> chunked cross-cov + solve_triangular) on host."""
+    from oracle import gp_ref
+    import scipy.linalg as sla
+    t0 = time.perf_counter()
+    G = gp_ref.gram_ardse(X, beta, s, delta)
+    L = np.linalg.cholesky(G)
+    alpha = sla.cho_solve((L, True), y)
+    t_fact = time.perf_counter() - t0
+    chunk, done, t_pred = 2000, 0, 0.0
+    means, vars_ = [], []
+    while done < Xs.shape[0] and (t_fact + t_pred) < budget_s:
+        t1 = time.perf_counter()
+        Ks = gp_ref.cross_ardse(Xs[done:done + chunk], X, beta, s)
+        mu = Ks @ alpha
+        V = sla.solve_triangular(L, Ks.T, lower=True, check_finite=False)
+        var = s - np.einsum("ij,ij->j", V, V)
+        t_pred += time.perf_counter() - t1
+        means.append(mu)
+        vars_.append(var)
+        done += Ks.shape[0]
+    m = Xs.shape[0]
+    t_full = t_fact + t_pred / done * m
+    # "reference-faithful": re-factorise per batch of 4 points (assess_all_models.py:481-489)
+    t2 = time.perf_counter()
+    G4 = gp_ref.gram_ardse(X, beta, s, delta)
+    L4 = np.linalg.cholesky(G4)
+    a4 = sla.cho_solve((L4, True), y)
+    K4 = gp_ref.cross_ardse(Xs[:4], X, beta, s)
+    _ = K4 @ a4, sla.solve_triangular(L4, K4.T, lower=True)
+    t4 = time.perf_counter() - t2
+    return {
+        "value": m / t_full, "unit": "predictions/s", "cores": _CPU_THREADS, "kind": "port",
+        "sample": (f"oracle/gp_ref numpy fp64 (OpenBLAS, {_CPU_THREADS} threads, "
+                   f"{platform.processor() or platform.machine()}): full n={X.shape[0]} "
+                   f"Gram+Cholesky ({t_fact:.2f} s) + predict on the first {done} of {m} test "
+                   f"points ({t_pred:.2f} s), extrapolated linearly to m={m}"),
+        "reference_faithful_value": 4.0 / t4,
+        "reference_faithful_sample": ("re-factorise per batch of 4 test points as "
+                                      "assess_all_models.py:481-489 does: one batch timed "
+                                      f"({t4:.2f} s)"),
+    }, np.concatenate(means), np.concatenate(vars_)
+
+
+def read_prof(pid):
+    import ctypes
+    cnt, tot, mx = ctypes.c_int(0), ctypes.c_double(0), ctypes.c_double(0)
+    _capi.call("gp_profile_read", pid, ctypes.addressof(cnt), ctypes.addressof(tot),
+               ctypes.addressof(mx))
+    return cnt.value, tot.value
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--m", type=int, default=100000, help="test points per GPU")
+    ap.add_argument("--d", type=int, default=8)
+    ap.add_argument("--m-chunk", type=int, default=0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds for the CPU leg")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    ctx = gdist.init_from_env("cuda")
+    dev = ctx.device
+    n, m, d = args.n, args.m, args.d
+    X, y, beta, Xs, s, delta = c3_inputs(ctx.rank, n, m, d)
+    Xd = torch.as_tensor(X, device=dev)
+    Xsd = torch.as_tensor(Xs, device=dev)
+    yd = torch.as_tensor(y, device=dev).reshape(1, n)
+    bd = torch.as_tensor(beta, device=dev).reshape(1, d)
+    sd = torch.tensor([s], dtype=torch.float64, device=dev)
+    dd = torch.tensor([delta], dtype=torch.float64, device=dev)
+    ws = kernels.PredictWorkspace()
+    mean = torch.empty((1, m), dtype=torch.float64, device=dev)
+    var = torch.empty((1, m), dtype=torch.float64, device=dev)
+
+    def step():
+        G = kernels.gram(Xd, bd, sd, dd)
+        ch = kernels.cholesky_inverse(G)
+        kernels.predict(ch, Xd, Xsd, bd, sd, sd, yd, m_chunk=args.m_chunk, workspace=ws,
+                        out=(mean, var))
+        return ch
+
+    for _ in range(args.warmup):
+        ch = step()
+    torch.cuda.synchronize()
+    ch.check()
+    _capi.call("gp_profile_enable", 64 * (args.steps + 1))
+    _capi.call("gp_profile_reset")
+
+    gdist.barrier(ctx)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    gdist.barrier(ctx)
+    elapsed = time.perf_counter() - t0
+    elapsed = gdist.max_over_ranks(ctx, elapsed)
+
+    prof = {k: read_prof(v) for k, v in (("trmm", _capi.PROF_TRMM), ("gram", _capi.PROF_GRAM),
+                                         ("potrf", _capi.PROF_POTRF),
+                                         ("cross", _capi.PROF_CROSS))}
+    _capi.call("gp_profile_enable", 0)
+
+    if ctx.rank != 0:
+        return
+    K = args.steps
+    value = ctx.world * m * K / elapsed
+    # algorithmic work: trmm n^2 + mean/var 4n flop per prediction
+    tr_cnt, tr_ms = prof["trmm"]
+    tr_flops = float(m) * K * (n * n + 4 * n)
+    tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12
+    roof = {"kernel": "trmm_reduce_kernel", "bound": "mfma", "achieved": round(tr_tfs, 3),
+            "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
+            "traffic": None, "launches": tr_cnt,
+            "avg_launch_ms": round(tr_ms / max(tr_cnt, 1), 4),
+            "flop_per_launch": tr_flops / max(tr_cnt, 1),
+            "work_note": "n^2 + 4n flop per prediction (lower-triangular L^-1 K*^T + mean/var)"}
+    g_cnt, g_ms = prof["gram"]
+    g_bytes = (8.0 * n * n + 8.0 * n * d) * g_cnt
+    p_cnt, p_ms = prof["potrf"]
+    p_flops = 2.0 * n ** 3 / 3.0 * p_cnt
+    c_cnt, c_ms = prof["cross"]
+    npad = kernels.padded_n(n)
+    c_bytes = 8.0 * npad * m * K
+    aux = {
+        "gram": {"bound": "hbm", "achieved": round(g_bytes / (g_ms * 1e-3) / 1e9, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(g_bytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                 "avg_launch_ms": round(g_ms / max(g_cnt, 1), 4)},
+        "potrf_inv": {"bound": "mfma", "achieved": round(p_flops / (p_ms * 1e-3) / 1e12, 3),
+                      "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": round(p_flops / (p_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                      "avg_call_ms": round(p_ms / max(p_cnt, 1), 4),
+                      "work_note": "potrf n^3/3 + triangular inverse n^3/3"},
+        "cross": {"bound": "hbm", "achieved": round(c_bytes / (c_ms * 1e-3) / 1e9, 1),
+                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(c_bytes / (c_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                  "ms_per_step": round(c_ms / K, 4)},
+        "trmm_ms_per_step": round(tr_ms / K, 4),
+    }
+    line = {
+        "metric": METRIC, "value": value, "unit": "predictions/s", "n_gpus": ctx.world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (SURVEY §8d C3 recipe: seeded uniform design, sin target)",
+        "config": {"workload": "C3 single-output ARD-SE GP: Gram + Cholesky/L^-1 + predict",
+                   "n_train": n, "m_test_per_gpu": m, "d": d,
+                   "parallelism": f"test-point shards x{ctx.world}, redundant factorisation"},
+        "roofline": roof, "roofline_aux": aux, "cpu_baseline": None,
+    }
+    if ctx.world == 1 and not args.no_cpu:
+        cb, mu_ref, var_ref = cpu_baseline(X, y, beta, Xs, s, delta, args.cpu_budget)
+        k = mu_ref.shape[0]
+        mu_g = mean[0, :k].cpu().numpy()
+        var_g = var[0, :k].cpu().numpy()
+        cb["parity_vs_gpu"] = {"points": int(k),
+                               "max_abs_dmean": float(np.max(np.abs(mu_g - mu_ref))),
+                               "max_abs_dvar": float(np.max(np.abs(var_g - var_ref)))}
+        line["cpu_baseline"] = cb
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

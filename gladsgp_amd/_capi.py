@@ -40,7 +40,12 @@ SIGNATURES = {
                         c_void_p]),
     "gp_nll": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p,
                        c_void_p, c_int, c_void_p]),
+    "gp_profile_enable": (c_int, [c_int]),
+    "gp_profile_reset": (c_int, []),
+    "gp_profile_read": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
 }
+
+PROF_GRAM, PROF_POTRF, PROF_TRMM, PROF_CROSS = 0, 1, 2, 3
 
 
 class GPFitUnavailable(RuntimeError):

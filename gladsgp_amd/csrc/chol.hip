@@ -16,6 +16,7 @@
 // operands staged into LDS k-major ([k][x], row pitch 65 doubles to spread banks), result
 // transposed through LDS so global stores are coalesced down columns.
 #include "gpfit_common.h"
+#include "gpfit_profile.h"
 #include "../../include/gpfit.h"
 
 namespace {
@@ -249,6 +250,7 @@ extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double
     GP_CK(hipMemset2DAsync(Linv + b * strideInv, sizeof(double) * ldinv, 0,
                            sizeof(double) * npad, npad, stream));
   const int N = gp_ceil_div(n, NB);
+  gpfit_prof_begin(GP_PROF_POTRF, stream);
   for (int k = 0; k < N; ++k) {
     hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, stream, A, lda, strideA,
                        Linv, ldinv, strideInv, n, k, info, logdet);
@@ -266,6 +268,7 @@ extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double
       GP_CK(hipGetLastError());
     }
   }
+  gpfit_prof_end(GP_PROF_POTRF, stream);
 #undef GP_CK
   return 0;
 }

@@ -11,6 +11,7 @@
 // one f64 exp (~1.3 T exp/s chip-wide, probe_f64) per element — the store stream (≈6 TB/s =
 // 0.75 T elements/s) is the bound.
 #include "gpfit_common.h"
+#include "gpfit_profile.h"
 #include "../../include/gpfit.h"
 
 namespace {
@@ -117,8 +118,10 @@ extern "C" int gp_gram_ardse(const double* X, int n, int d, int ldx, const doubl
   if (batch > 1 && strideG < (long long)ldg * n) return -11;
   if (batch < 0) return -12;
   if (n == 0 || batch == 0) return 0;
+  gpfit_prof_begin(GP_PROF_GRAM, stream);
   hipError_t e = gpfit_ardse_launch(X, n, ldx, X, n, ldx, d, beta, ldbeta, s, delta, G, ldg,
                                     strideG, n, n, batch, stream);
+  gpfit_prof_end(GP_PROF_GRAM, stream);
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }
 

@@ -17,6 +17,7 @@
 //   3. finalize           mean = sum_I pm, var = s_pred - sum_I pv
 // z = X w is a small lower-triangular gemv (linalg.hip trmv_kernel).
 #include "gpfit_common.h"
+#include "gpfit_profile.h"
 #include "../../include/gpfit.h"
 
 hipError_t gpfit_ardse_launch(const double* XA, int na, int ldxa, const double* XB, int nb,
@@ -248,12 +249,16 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
   for (int ch = 0; ch < p.nchunks; ++ch) {
     const int c0 = ch * p.mc;
     const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
+    gpfit_prof_begin(GP_PROF_CROSS, stream);
     GP_CK(gpfit_ardse_launch(X, n, ldx, Xs + (long long)c0 * ldxs, mv, ldxs, d, beta, ldbeta,
                              s, nullptr, kt, p.npad, sK, p.npad, p.mc, batch, stream));
+    gpfit_prof_end(GP_PROF_CROSS, stream);
     const int ncol_tiles = gp_ceil_div(mv, BC);
+    gpfit_prof_begin(GP_PROF_TRMM, stream);
     hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0,
                        stream, Linv, ldinv, strideInv, kt, p.npad, sK, z, p.npad, part, p.NI,
                        ncol_tiles, p.mc);
+    gpfit_prof_end(GP_PROF_TRMM, stream);
     GP_CK(hipGetLastError());
     hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0,
                        stream, part, p.NI, p.mc, mv, s_pred, mean, var, ldo, c0);

@@ -117,6 +117,21 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
            const double* w, int ldw, const double* logdet, double* nll, double* work,
            int batch, hipStream_t stream);
 
+/*
+ * Optional kernel timing (diagnostics; not part of the reference surface).  When enabled with
+ * capacity > 0, instrumented launches record a hipEvent pair on their own stream; after the
+ * stream has drained, gp_profile_read returns the number of recorded launches of kernel `id`
+ * and their summed / largest device time in milliseconds.  Host-side, single-threaded use.
+ */
+#define GP_PROF_GRAM 0        /* gram / cross-covariance build (ardse_kernel)            */
+#define GP_PROF_POTRF 1       /* whole gp_potrf_inv sequence                             */
+#define GP_PROF_TRMM 2        /* predict: trmm_reduce_kernel (dominant kernel)           */
+#define GP_PROF_CROSS 3       /* predict: per-chunk cross-covariance build               */
+#define GP_PROF_NUM 4
+int gp_profile_enable(int capacity);
+int gp_profile_reset(void);
+int gp_profile_read(int id, int* count, double* total_ms, double* max_ms);
+
 #ifdef __cplusplus
 }
 #endif
