@@ -2,19 +2,22 @@
 //
 // Reference behaviour replaced: the SPD factorisation inside SEPIA's likelihood / prediction
 // (LAPACK potrf), scipy.linalg.cholesky(lower=True) in examples/01...ipynb:66,144 and GPmodule's
-// K_inv (examples/02...ipynb:232-233).  LAPACK semantics: info = first failing pivot (1-based).
+// K_inv (examples/02...ipynb:232-233).  LAPACK semantics: info = first failing pivot (1-based),
+// the strict upper triangle of A is neither read nor written.
 //
 // Algorithm (NB = 64 blocks, k = 0..N-1), X = L^-1 built alongside L:
-//   diag   : L_kk = chol(A_kk) in LDS, D_k = L_kk^-1 (written as X_kk), logdet += 2 sum log
+//   diag   : L_kk = chol(A_kk), D_k = L_kk^-1 (written as X_kk), logdet += 2 sum log L_ii
 //   panel  : L_ik = A_ik D_k^T            (i > k)        — 64^3 MFMA tile GEMMs
 //            X_kc = D_k R_kc              (c < k)        — R_kc accumulated in X's storage
 //   update : A_ij -= L_ik L_jk^T          (k < j <= i)   — SYRK/GEMM trailing update
-//            R_ic -= L_ik X_kc            (i > k, c<=k)  — drives the block forward
-//                                                          substitution of L X = I
-// Both products are n^3/3 flop; every tile product runs on v_mfma_f64_16x16x4_f64.
-// Tile GEMM: 256 threads = 4 waves in a 2x2 grid of 32x32 sub-tiles (2x2 MFMA 16x16 each);
-// operands staged into LDS k-major ([k][x], row pitch 65 doubles to spread banks), result
-// transposed through LDS so global stores are coalesced down columns.
+//            R_ic -= L_ik X_kc            (i > k, c<=k)  — block forward substitution of L X = I
+// Lookahead: the update block that owns tile (k+1, k+1) factors and inverts it right after its
+// own update (diag_factor_inv below), so each step is two launches (panel, update+diag) and the
+// serial diagonal work overlaps the rest of the trailing update.
+//
+// diag_factor_inv: one 256-thread block, register resident (see the function for the scheme):
+// X = L^-1 comes out of the same right-looking sweep as L (X_j. = R_j. / L_jj,
+// R_i. -= L_ij X_j.), one barrier and 32 FMAs per thread per column step.
 #include "gpfit_common.h"
 #include "gpfit_profile.h"
 #include "../../include/gpfit.h"
@@ -23,6 +26,18 @@ namespace {
 
 constexpr int NB = 64;
 constexpr int LP = NB + 1;  // LDS pitch (doubles)
+
+struct __align__(16) Smem {
+  double As[NB * LP];
+  double Bs[NB * LP];
+  double VA[2][NB];    // scaled L column of the current step (zeros at and above the pivot)
+  double RR[2][NB];    // unscaled R row of the current step
+  double sps[NB];      // L_jj
+  double invs[NB];     // 1 / L_jj
+  double inv[2];
+  double red[4];
+  int fail;
+};
 
 // S[k][x]: NAT → src[x + k*ld] (x contiguous), TRN → src[k + x*ld] (k contiguous).
 template <bool TRN>
@@ -61,14 +76,10 @@ GP_DEV void mma64(const double* As, const double* Bs, f64x4 (&acc)[2][2]) {
   }
 }
 
-// Write the block's 64x64 accumulator to C (column-major, ld), rows < rv, cols < cv.
-// SUB: C -= acc, else C = acc.  LOWER: only row >= col (diagonal tiles of A).
-template <bool SUB>
-GP_DEV void epilogue(double* Cs, const f64x4 (&acc)[2][2], double* __restrict__ C, int ld,
-                     int rv, int cv, bool lower) {
+// Scatter the block's accumulator into LDS as Cs[col][row] (pitch LP).
+GP_DEV void acc_to_lds(double* Cs, const f64x4 (&acc)[2][2]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
-  __syncthreads();  // all waves done reading As/Bs (Cs aliases As)
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -78,15 +89,168 @@ GP_DEV void epilogue(double* Cs, const f64x4 (&acc)[2][2], double* __restrict__ 
         const int row = wr * 32 + mi * 16 + lk + 4 * r, col = wc * 32 + nj * 16 + li;
         Cs[col * LP + row] = acc[mi][nj][r];
       }
+}
+
+// Coalesced tile element owned by thread for slot q: row = g & 63, col = g >> 6.
+GP_DEV void slot_rc(int q, int& row, int& col) {
+  const int g = threadIdx.x + 256 * q;
+  row = g & (NB - 1);
+  col = g >> 6;
+}
+
+// C = acc (STORE) for rows < rv, cols < cv.
+GP_DEV void store_tile(double* Cs, const f64x4 (&acc)[2][2], double* __restrict__ C, int ld,
+                       int rv, int cv) {
+  __syncthreads();  // all waves done with As/Bs (Cs aliases As)
+  acc_to_lds(Cs, acc);
   __syncthreads();
 #pragma unroll 4
-  for (int q = 0; q < (NB * NB) / 256; ++q) {
-    const int g = threadIdx.x + 256 * q;
-    const int row = g & (NB - 1), col = g >> 6;
-    if (row < rv && col < cv && (!lower || row >= col)) {
-      double* p = C + row + (long long)col * ld;
-      const double v = Cs[col * LP + row];
-      *p = SUB ? (*p - v) : v;
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    if (row < rv && col < cv) C[row + (long long)col * ld] = Cs[col * LP + row];
+  }
+}
+
+// Factor + invert the 64x64 tile held (full, symmetric) in T[row * LP + col]; nb valid rows
+// (rows/cols >= nb are identity padding).  On return T holds L (lower) and U holds L^-1
+// (lower, zero upper); returns 0 or the 1-based local index of the first non-PD pivot.
+//
+// Thread t owns row i = t & 63 and the 16 contiguous columns c = 16 cq + u (cq = t >> 6,
+// wave-uniform) of A and of R (R starts as I).  Step j needs only
+//   VA[c] = L[c][j] = A[c][j] / L[j][j]  (zero for c <= j)   and   RR[c] = R[j][c] (zero c > j)
+// so the update is 32 unconditional FMAs per thread:
+//   A[i][c] -= L[i][j] VA[c],   R[i][c] -= (L[i][j] / L[j][j]) RR[c]
+// (finalised L columns / R entries see zeros and stay put; X = L^-1 rows are R rows / L_ii and
+// the L columns are kept unscaled until the end).  The wave owning column j+1 computes the next
+// pivot from its own registers and publishes VA for step j+1; lane j+1 of every wave publishes
+// its slice of R row j+1 — one barrier per step, ping-pong buffers, no selects in the loop.
+GP_DEV int diag_factor_inv(Smem& sm, double* T, double* U, int nb, double* ld_out) {
+  const int tid = threadIdx.x;
+  const int i = tid & (NB - 1);
+  const int cq = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cb = cq * 16;
+  double a[16], r[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    a[u] = T[i * LP + cb + u];
+    r[u] = (cb + u == i) ? 1.0 : 0.0;
+  }
+  // publish step 0: column 0 is owned by wave 0 (u = 0), row 0 of R = e_0
+  if (tid == 0) sm.fail = 0;
+  if (cq == 0) {
+    const double piv = readlane_f64(a[0], 0);
+    const bool bad = !(piv > 0.0) || !isfinite(piv);
+    const double inv = rsqrt_nr(piv), sp = piv * inv;
+    sm.VA[0][i] = (i > 0) ? a[0] * inv : 0.0;
+    if (i == 0) {
+      sm.inv[0] = inv;
+      sm.sps[0] = sp;
+      sm.invs[0] = inv;
+      if (bad) sm.fail = 1;
+    }
+  }
+  if (i == 0) {
+#pragma unroll
+    for (int u = 0; u < 16; u += 2) {
+      double2 y;
+      y.x = r[u];
+      y.y = r[u + 1];
+      *reinterpret_cast<double2*>(&sm.RR[0][cb + u]) = y;
+    }
+  }
+  bool stop = false;
+#pragma unroll 1
+  for (int jb = 0; jb < NB / 16 && !stop; ++jb) {
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int j = jb * 16 + jj;
+      const int p = jj & 1, q = p ^ 1;
+      __syncthreads();
+      if (sm.fail) { stop = true; break; }
+      const double inv = sm.inv[p];
+      const double lij = sm.VA[p][i];
+      const double l2 = lij * inv;
+#pragma unroll
+      for (int u = 0; u < 16; u += 2) {
+        const double2 va = *reinterpret_cast<const double2*>(&sm.VA[p][cb + u]);
+        const double2 rr = *reinterpret_cast<const double2*>(&sm.RR[p][cb + u]);
+        a[u] = fma(-lij, va.x, a[u]);
+        a[u + 1] = fma(-lij, va.y, a[u + 1]);
+        r[u] = fma(-l2, rr.x, r[u]);
+        r[u + 1] = fma(-l2, rr.y, r[u + 1]);
+      }
+      if (j + 1 < NB) {
+        // column j+1: owner wave and register slot are compile-time per jj.  The pivot chain
+        // (readlane -> rsqrt -> publish) is the step's critical path; it is straight-line code
+        // in every wave, only the owner's stores are predicated.
+        const int own = (jj < 15) ? jb : jb + 1;
+        const int uo = (jj + 1) & 15;
+        const double piv = readlane_f64(a[uo], j + 1);
+        const double inv1 = rsqrt_nr(piv), sp = piv * inv1;
+        if (cq == own) {
+          const bool bad = !(piv > 0.0) || !isfinite(piv);
+          sm.VA[q][i] = (i > j + 1) ? a[uo] * inv1 : 0.0;
+          if (i == 0) {
+            sm.inv[q] = inv1;
+            sm.sps[j + 1] = sp;
+            sm.invs[j + 1] = inv1;
+            if (bad) sm.fail = j + 2;
+          }
+        }
+        if (i == j + 1) {
+#pragma unroll
+          for (int u = 0; u < 16; u += 2) {
+            double2 y;
+            y.x = r[u];
+            y.y = r[u + 1];
+            *reinterpret_cast<double2*>(&sm.RR[q][cb + u]) = y;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int f = sm.fail;
+  if (f) return (f <= nb) ? f : 0;
+  const double inv_i = sm.invs[i];
+  double lg = 0.0;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int c = cb + u;
+    T[i * LP + c] = (c < i) ? a[u] * sm.invs[c] : ((c == i) ? sm.sps[i] : 0.0);
+    U[i * LP + c] = (c <= i) ? r[u] * inv_i : 0.0;
+  }
+  if (cq == 0 && i < nb) lg = 2.0 * log(sm.sps[i]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
+  if ((tid & 63) == 0) sm.red[tid >> 6] = lg;
+  __syncthreads();
+  if (ld_out) *ld_out = (sm.red[0] + sm.red[1]) + (sm.red[2] + sm.red[3]);
+  return 0;
+}
+
+// Factor diagonal block k whose (updated, symmetric) tile is in sm.As as [row][col]; write
+// L_kk into A, D_k into X, accumulate logdet, set info.
+GP_DEV void diag_block(Smem& sm, double* __restrict__ Ab, int lda, double* __restrict__ Xb,
+                       int ldx, int n, int k, int* info, double* logdet, int b) {
+  const int k0 = k * NB, nb = min(NB, n - k0);
+  double lg = 0.0;
+  const int f = diag_factor_inv(sm, sm.As, sm.Bs, nb, &lg);
+  if (f) {
+    if (threadIdx.x == 0 && info) info[b] = k0 + f;
+    return;
+  }
+  if (threadIdx.x == 0 && logdet) logdet[b] += lg;
+  double* Akk = Ab + k0 + (long long)k0 * lda;
+  double* Xkk = Xb + k0 + (long long)k0 * ldx;
+#pragma unroll 4
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    if (row < nb && col < nb) {
+      if (row >= col) Akk[row + (long long)col * lda] = sm.As[row * LP + col];
+      Xkk[row + (long long)col * ldx] = sm.Bs[row * LP + col];
     }
   }
 }
@@ -96,62 +260,23 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(
     long long sX, int n, int k, int* __restrict__ info, double* __restrict__ logdet) {
   const int b = blockIdx.x;
   if (info && info[b] != 0) return;
-  __shared__ double T[NB * LP];
-  __shared__ double U[NB * LP];
-  const int k0 = k * NB;
-  const int nb = min(NB, n - k0);
-  double* Ab = A + b * sA + k0 + (long long)k0 * lda;
-  double* Xb = X + b * sX + k0 + (long long)k0 * ldx;
-  const int tid = threadIdx.x;
-  // T[i][c] row-major in LDS (i = row): coalesced read down columns of A.
-  for (int g = tid; g < NB * NB; g += 256) {
-    const int i = g & (NB - 1), c = g >> 6;
+  __shared__ Smem sm;
+  const int k0 = k * NB, nb = min(NB, n - k0);
+  double* Ab = A + b * sA;
+  const double* Akk = Ab + k0 + (long long)k0 * lda;
+  // symmetric tile from the lower triangle only (upper triangle of A is never read)
+  for (int g = threadIdx.x; g < NB * NB; g += 256) {
+    const int row = g & (NB - 1), col = g >> 6;
     double v;
-    if (i < nb && c < nb) v = Ab[i + (long long)c * lda];
-    else v = (i == c) ? 1.0 : 0.0;   // identity padding keeps the edge block SPD
-    T[i * LP + c] = v;
+    if (row < nb && col < nb) {
+      v = (row >= col) ? Akk[row + (long long)col * lda] : Akk[col + (long long)row * lda];
+    } else {
+      v = (row == col) ? 1.0 : 0.0;
+    }
+    sm.As[row * LP + col] = v;
   }
   __syncthreads();
-  const int row = tid & (NB - 1), cq = tid >> 6;
-  for (int j = 0; j < NB; ++j) {
-    const double piv = T[j * LP + j];
-    if (!(piv > 0.0) || !isfinite(piv)) {  // uniform: every thread reads the same LDS word
-      if (tid == 0 && j < nb && info) { info[b] = k0 + j + 1; }
-      return;
-    }
-    const double sp = sqrt(piv);
-    __syncthreads();  // everyone has read the pivot before it is overwritten
-    if (tid == j) T[j * LP + j] = sp;
-    if (tid > j && tid < NB) T[tid * LP + j] /= sp;
-    __syncthreads();
-    for (int c = j + 1 + cq; c <= row; c += 4) T[row * LP + c] -= T[row * LP + j] * T[c * LP + j];
-    __syncthreads();
-  }
-  // D = L^-1 : thread c solves column c by forward substitution (its own column only).
-  if (tid < NB) {
-    const int c = tid;
-    for (int i = 0; i < NB; ++i) {
-      if (i < c) { U[i * LP + c] = 0.0; continue; }
-      double acc = (i == c) ? 1.0 : 0.0;
-      for (int p = c; p < i; ++p) acc -= T[i * LP + p] * U[p * LP + c];
-      U[i * LP + c] = acc / T[i * LP + i];
-    }
-  }
-  // logdet contribution (wave 0)
-  if (tid < 64 && logdet) {
-    double v = (tid < nb) ? 2.0 * log(T[tid * LP + tid]) : 0.0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (tid == 0) logdet[b] += v;
-  }
-  __syncthreads();
-  for (int g = tid; g < NB * NB; g += 256) {
-    const int i = g & (NB - 1), c = g >> 6;
-    if (i < nb && c < nb) {
-      if (i >= c) Ab[i + (long long)c * lda] = T[i * LP + c];
-      Xb[i + (long long)c * ldx] = U[i * LP + c];
-    }
-  }
+  diag_block(sm, Ab, lda, X + b * sX, ldx, n, k, info, logdet, b);
 }
 
 __global__ __launch_bounds__(256) void chol_panel_kernel(
@@ -159,8 +284,7 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
     long long sX, int n, int k, int nbelow, const int* __restrict__ info) {
   const int b = blockIdx.y;
   if (info && info[b] != 0) return;
-  __shared__ double As[NB * LP];
-  __shared__ double Bs[NB * LP];
+  __shared__ Smem sm;
   const int k0 = k * NB, kv = min(NB, n - k0);
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
@@ -170,59 +294,117 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
     // L_ik = A_ik D_k^T :  opA[r][p] = A_ik(r,p) (NAT), opB[p][c] = D_k(c,p) (NAT)
     const int i0 = (k + 1 + blockIdx.x) * NB, rv = min(NB, n - i0);
     double* Aik = Ab + i0 + (long long)k0 * lda;
-    stage<false>(As, Aik, lda, rv, kv);
-    stage<false>(Bs, Dk, ldx, kv, kv);
+    stage<false>(sm.As, Aik, lda, rv, kv);
+    stage<false>(sm.Bs, Dk, ldx, kv, kv);
     __syncthreads();
-    mma64(As, Bs, acc);
-    epilogue<false>(As, acc, Aik, lda, rv, kv, false);
+    mma64(sm.As, sm.Bs, acc);
+    store_tile(sm.As, acc, Aik, lda, rv, kv);
   } else {
     // X_kc = D_k R_kc :  opA[r][p] = D_k(r,p) (NAT), opB[p][c] = R_kc(p,c) (TRN)
     const int c0 = (blockIdx.x - nbelow) * NB;
     double* Rkc = Xb + k0 + (long long)c0 * ldx;
-    stage<false>(As, Dk, ldx, kv, kv);
-    stage<true>(Bs, Rkc, ldx, NB, kv);
+    stage<false>(sm.As, Dk, ldx, kv, kv);
+    stage<true>(sm.Bs, Rkc, ldx, NB, kv);
     __syncthreads();
-    mma64(As, Bs, acc);
-    epilogue<false>(As, acc, Rkc, ldx, kv, NB, false);
+    mma64(sm.As, sm.Bs, acc);
+    store_tile(sm.As, acc, Rkc, ldx, kv, NB);
   }
 }
 
+// Trailing update of step k.  Block 0 owns tile (k+1, k+1) and then factors it (lookahead).
 __global__ __launch_bounds__(256) void chol_update_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
-    long long sX, int n, int k, int T, const int* __restrict__ info) {
+    long long sX, int n, int k, int T, int* __restrict__ info, double* __restrict__ logdet) {
   const int b = blockIdx.y;
   if (info && info[b] != 0) return;
-  __shared__ double As[NB * LP];
-  __shared__ double Bs[NB * LP];
+  __shared__ Smem sm;
   const int k0 = k * NB, kv = min(NB, n - k0);
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
   const int ntri = T * (T + 1) / 2;
   const int idx = blockIdx.x;
-  f64x4 acc[2][2];
+  double* Cp;
+  int ldc, rv, cv, ldb;
+  bool diag = false, trn;
+  const double *Ap, *Bp;
   if (idx < ntri) {
     int ii = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
     while (ii * (ii + 1) / 2 > idx) --ii;
     while ((ii + 1) * (ii + 2) / 2 <= idx) ++ii;
     const int jj = idx - ii * (ii + 1) / 2;
     const int i0 = (k + 1 + ii) * NB, j0 = (k + 1 + jj) * NB;
-    const int rv = min(NB, n - i0), cv = min(NB, n - j0);
-    // A_ij -= L_ik L_jk^T
-    stage<false>(As, Ab + i0 + (long long)k0 * lda, lda, rv, kv);
-    stage<false>(Bs, Ab + j0 + (long long)k0 * lda, lda, cv, kv);
-    __syncthreads();
-    mma64(As, Bs, acc);
-    epilogue<true>(As, acc, Ab + i0 + (long long)j0 * lda, lda, rv, cv, ii == jj);
+    rv = min(NB, n - i0);
+    cv = min(NB, n - j0);
+    Ap = Ab + i0 + (long long)k0 * lda;                 // L_ik
+    Bp = Ab + j0 + (long long)k0 * lda;                 // L_jk  (opB[p][c] = L_jk(c,p), NAT)
+    ldb = lda;
+    trn = false;
+    Cp = Ab + i0 + (long long)j0 * lda;
+    ldc = lda;
+    diag = (ii == jj);
   } else {
     const int idx2 = idx - ntri;
     const int ii = idx2 / (k + 1), c = idx2 % (k + 1);
-    const int i0 = (k + 1 + ii) * NB, c0 = c * NB, rv = min(NB, n - i0);
-    // R_ic -= L_ik X_kc :  opB[p][cc] = X(k0+p, c0+cc) (TRN)
-    stage<false>(As, Ab + i0 + (long long)k0 * lda, lda, rv, kv);
-    stage<true>(Bs, Xb + k0 + (long long)c0 * ldx, ldx, NB, kv);
+    const int i0 = (k + 1 + ii) * NB, c0 = c * NB;
+    rv = min(NB, n - i0);
+    cv = NB;
+    Ap = Ab + i0 + (long long)k0 * lda;                 // L_ik
+    Bp = Xb + k0 + (long long)c0 * ldx;                 // X_kc (opB[p][cc] = X(k0+p,c0+cc), TRN)
+    ldb = ldx;
+    trn = true;
+    Cp = Xb + i0 + (long long)c0 * ldx;
+    ldc = ldx;
+  }
+  // prefetch the C tile (coalesced) while the operands are staged
+  double cpre[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    const bool ok = row < rv && col < cv && (!diag || row >= col);
+    cpre[q] = ok ? Cp[row + (long long)col * ldc] : 0.0;
+  }
+  stage<false>(sm.As, Ap, lda, rv, kv);
+  if (trn) stage<true>(sm.Bs, Bp, ldb, NB, kv);
+  else stage<false>(sm.Bs, Bp, ldb, cv, kv);
+  __syncthreads();
+  f64x4 acc[2][2];
+  mma64(sm.As, sm.Bs, acc);
+  __syncthreads();
+  acc_to_lds(sm.As, acc);      // As[col][row] = product
+  __syncthreads();
+  if (idx == 0) {
+    // tile (k+1, k+1): updated lower values -> symmetric [row][col] tile in As, then factor
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int row, col;
+      slot_rc(q, row, col);
+      cpre[q] -= sm.As[col * LP + row];
+    }
     __syncthreads();
-    mma64(As, Bs, acc);
-    epilogue<true>(As, acc, Xb + i0 + (long long)c0 * ldx, ldx, rv, NB, false);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int row, col;
+      slot_rc(q, row, col);
+      if (row < rv && col < cv) {
+        if (row >= col) {
+          sm.As[row * LP + col] = cpre[q];
+          sm.As[col * LP + row] = cpre[q];
+        }
+      } else {
+        sm.As[row * LP + col] = (row == col) ? 1.0 : 0.0;
+      }
+    }
+    __syncthreads();
+    diag_block(sm, Ab, lda, Xb, ldx, n, k + 1, info, logdet, b);
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    if (row < rv && col < cv && (!diag || row >= col))
+      Cp[row + (long long)col * ldc] = cpre[q] - sm.As[col * LP + row];
   }
 }
 
@@ -251,10 +433,10 @@ extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double
                            sizeof(double) * npad, npad, stream));
   const int N = gp_ceil_div(n, NB);
   gpfit_prof_begin(GP_PROF_POTRF, stream);
+  hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, stream, A, lda, strideA,
+                     Linv, ldinv, strideInv, n, 0, info, logdet);
+  GP_CK(hipGetLastError());
   for (int k = 0; k < N; ++k) {
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, stream, A, lda, strideA,
-                       Linv, ldinv, strideInv, n, k, info, logdet);
-    GP_CK(hipGetLastError());
     const int T = N - k - 1;
     if (T + k > 0) {
       hipLaunchKernelGGL(chol_panel_kernel, dim3(T + k, batch), dim3(256), 0, stream, A, lda,
@@ -264,7 +446,7 @@ extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double
     if (T > 0) {
       const int nt = T * (T + 1) / 2 + T * (k + 1);
       hipLaunchKernelGGL(chol_update_kernel, dim3(nt, batch), dim3(256), 0, stream, A, lda,
-                         strideA, Linv, ldinv, strideInv, n, k, T, info);
+                         strideA, Linv, ldinv, strideInv, n, k, T, info, logdet);
       GP_CK(hipGetLastError());
     }
   }

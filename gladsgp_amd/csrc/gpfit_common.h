@@ -18,6 +18,32 @@ GP_DEV f64x4 mfma16x16x4(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// Broadcast lane 0's double to an SGPR pair: tells the compiler a value is wave-uniform.
+GP_DEV double uniform_f64(double x) {
+  const unsigned long long u = __double_as_longlong(x);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// v_readlane of a double: lane `l` (wave-uniform index) broadcast through SGPRs.
+GP_DEV double readlane_f64(double x, int l) {
+  const unsigned long long u = __double_as_longlong(x);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// 1/sqrt(x) for x > 0: hardware v_rsq_f64 estimate + two Newton steps (<= 1 ulp typical);
+// a short dependent chain, used where the pivot sits on a sequential critical path.
+GP_DEV double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * fma(-hx * y, y, 1.5);
+  y = y * fma(-hx * y, y, 1.5);
+  return y;
+}
+
 GP_DEV f64x4 zero4() { f64x4 z = {0.0, 0.0, 0.0, 0.0}; return z; }
 
 // Squared ARD distance sum_k beta_k (a_k - b_k)^2 ; D is a compile-time dimension bound.

@@ -8,26 +8,38 @@
 
 namespace {
 
-// z_b[r] = sum_{k<=r, k<n} Linv_b[r,k] w_b[k] for r < rows; 256 threads = 64 rows x 4 slices.
-__global__ __launch_bounds__(256) void trmv_kernel(const double* __restrict__ Linv, int ld,
-                                                   long long sL, const double* __restrict__ w,
-                                                   int ldw, double* __restrict__ z, int ldz,
-                                                   int rows, int n) {
+// z_b[r] = sum_{k<=r, k<n} Linv_b[r,k] w_b[k] for r < rows.  1024 threads = 64 rows x 16
+// k-slices: each wave reads 64 consecutive rows of one column (512 B, coalesced), the 16
+// partial sums meet in LDS.  Reads the n^2/2 lower triangle once: HBM-bound.
+constexpr int kTrmvSlices = 16;
+__global__ __launch_bounds__(1024) void trmv_kernel(const double* __restrict__ Linv, int ld,
+                                                    long long sL, const double* __restrict__ w,
+                                                    int ldw, double* __restrict__ z, int ldz,
+                                                    int rows, int n) {
   const int b = blockIdx.y;
   const int r = blockIdx.x * 64 + (threadIdx.x & 63);
   const int ks = threadIdx.x >> 6;
   const double* L = Linv + b * sL;
   const double* wb = w + (long long)b * ldw;
-  double acc = 0.0;
-  const int kend = min(r + 1, n);
-  if (r < rows)
-    for (int k = ks; k < kend; k += 4) acc = fma(L[r + (long long)k * ld], wb[k], acc);
-  __shared__ double red[4][64];
-  red[ks][threadIdx.x & 63] = acc;
+  double acc0 = 0.0, acc1 = 0.0;
+  const int kend = min(blockIdx.x * 64 + 64, n);   // block-uniform bound; L is zero above r
+  if (r < rows) {
+    int k = ks;
+    for (; k + kTrmvSlices < kend; k += 2 * kTrmvSlices) {
+      acc0 = fma(L[r + (long long)k * ld], wb[k], acc0);
+      acc1 = fma(L[r + (long long)(k + kTrmvSlices) * ld], wb[k + kTrmvSlices], acc1);
+    }
+    if (k < kend) acc0 = fma(L[r + (long long)k * ld], wb[k], acc0);
+  }
+  __shared__ double red[kTrmvSlices][64];
+  red[ks][threadIdx.x & 63] = acc0 + acc1;
   __syncthreads();
   if (ks == 0 && r < rows) {
     const int t = threadIdx.x;
-    z[(long long)b * ldz + r] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < kTrmvSlices; ++q) s += red[q][t];
+    z[(long long)b * ldz + r] = s;
   }
 }
 
@@ -52,7 +64,7 @@ __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restric
 hipError_t gpfit_trmv_launch(const double* Linv, int ld, long long sL, const double* w,
                              int ldw, double* z, int ldz, int rows, int n, int batch,
                              hipStream_t st) {
-  hipLaunchKernelGGL(trmv_kernel, dim3(gp_ceil_div(rows, 64), batch), dim3(256), 0, st, Linv,
+  hipLaunchKernelGGL(trmv_kernel, dim3(gp_ceil_div(rows, 64), batch), dim3(1024), 0, st, Linv,
                      ld, sL, w, ldw, z, ldz, rows, n);
   return hipGetLastError();
 }

@@ -9,8 +9,8 @@
 // both; V is reduced in registers and never written.
 //
 // Per chunk of m_c test points:
-//   1. ardse (gram.hip)   Kt = s exp(-sum beta (X - Xs)^2), n_pad x m_c, column per test point
-//                         (exp evaluated once per element; HBM-write-bound)
+//   1. cross_kp           Kt = s exp(-sum beta (X - Xs)^2), n_pad x m_c, stored k-pair
+//                         interleaved for the TRMM's LDS image (exp once per element)
 //   2. trmm_reduce        for each 128x128 tile (I, C) of V: acc = sum_{k < 128(I+1)} X[I,k] Kt[k,C]
 //                         on v_mfma_f64_16x16x4_f64, epilogue: per-column partial sums of
 //                         acc*z and acc^2 -> part[b][I][col]  (MFMA-bound: n^2 m flop)
@@ -34,27 +34,101 @@ namespace {
 constexpr int BI = 128;   // V tile rows (L^-1 rows)
 constexpr int BC = 128;   // V tile cols (test points)
 constexpr int BK = 16;    // K step
-constexpr int PA = BI + 8;   // As pitch (doubles): [k][i]
-constexpr int PB = BK + 1;   // Bs pitch (doubles): [c][k]
 constexpr long long kDefaultChunkElems = 16ll << 20;   // ~128 MB of Kt per chunk (MALL-sized)
 
-// One 128x128 tile of V = Linv * Kt per block; 4 waves in 2x2, each 64x64 = 4x4 MFMA tiles.
-__global__ __launch_bounds__(256) void trmm_reduce_kernel(
-    const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt,
-    int ldk, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
-    int NI, int NC, int mc) {
+// Cross-covariance chunk in the k-pair-interleaved layout the TRMM streams:
+//   Kt2[((k >> 1) * mc + c) * 2 + (k & 1)] = s * exp(-sum beta (X[k] - Xs[c])^2)
+// (zero for k >= n or c >= mv).  Each thread owns one test point c (registers) and walks 32
+// k-pairs whose design rows are broadcast from LDS; it stores one 16-B pair per k-pair, so a
+// wave writes 1 KB contiguous per instruction.
+template <int D>
+__global__ __launch_bounds__(256) void cross_kp_kernel(
+    const double* __restrict__ X, int n, int ldx, const double* __restrict__ Xs, int mv,
+    int ldxs, int d, const double* __restrict__ beta, int ldbeta, const double* __restrict__ s,
+    double* __restrict__ Kt2, int mc, long long sK) {
+  const int b = blockIdx.z;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int kp0 = blockIdx.y * 32;
+  __shared__ double xk[64][D];
+  __shared__ double bs[D];
+  const double* bb = beta + (long long)b * ldbeta;
+  if (threadIdx.x < D) bs[threadIdx.x] = (threadIdx.x < d) ? bb[threadIdx.x] : 0.0;
+  for (int t = threadIdx.x; t < 64 * D; t += 256) {
+    const int kk = t / D, dd = t % D, k = 2 * kp0 + kk;
+    xk[kk][dd] = (k < n && dd < d) ? X[(long long)k * ldx + dd] : 0.0;
+  }
+  double xc[D];
+#pragma unroll
+  for (int dd = 0; dd < D; ++dd) xc[dd] = (c < mv && dd < d) ? Xs[(long long)c * ldxs + dd] : 0.0;
+  __syncthreads();
+  if (c >= mc) return;
+  const double sb = s[b];
+  double* o = Kt2 + (long long)b * sK;
+  const bool col_ok = c < mv;
+#pragma unroll 2
+  for (int kk = 0; kk < 32; ++kk) {
+    const int k = 2 * (kp0 + kk);
+    double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+    for (int dd = 0; dd < D; ++dd) {
+      const double t0 = xk[2 * kk][dd] - xc[dd], t1 = xk[2 * kk + 1][dd] - xc[dd];
+      e0 = fma(bs[dd] * t0, t0, e0);
+      e1 = fma(bs[dd] * t1, t1, e1);
+    }
+    double2 v;
+    v.x = (col_ok && k < n) ? sb * exp(-e0) : 0.0;
+    v.y = (col_ok && k + 1 < n) ? sb * exp(-e1) : 0.0;
+    *reinterpret_cast<double2*>(o + ((long long)(kp0 + kk) * mc + c) * 2) = v;
+  }
+}
+
+// One 128x128 tile of V = Linv * Kt per block, 4 waves in 2x2 (64x64 each = 4x4 MFMA tiles).
+// Operands stream straight into LDS with global_load_lds (16 B per lane), double-buffered:
+//   A step (16 k x 128 rows of L^-1): 16 rows of 1 KB, row pitch 1152 B (lanes 0-15 / 16-31
+//     of a fragment read land 32 banks apart: conflict-free)
+//   B step (8 k-pairs x 128 test points x 2): 2 KB per k-pair, already in the [kp][c][2]
+//     order of cross_kp_kernel, so a fragment read covers 256 contiguous bytes.
+// One barrier per K-step; ~69 KB of LDS and <= 256 VGPRs -> 2 blocks (8 waves) per CU.
+constexpr int APITCH = 144;                    // doubles per staged A row (1152 B)
+constexpr int ASTAGE = BK * APITCH;            // 2304 doubles
+constexpr int BSTAGE = (BK / 2) * BC * 2;      // 2048 doubles
+constexpr int STAGE = ASTAGE + BSTAGE;         // 4352 doubles = 34816 B
+
+GP_DEV void glds16(const double* g, double* l) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)l, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
+    const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt2,
+    int mc, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
+    int NI, int NC) {
+  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const int b = blockIdx.y;
   const int t = blockIdx.x;
   const int I = NI - 1 - t / NC;     // heaviest row tiles dispatch first
   const int C = t % NC;
-  const double* L = Linv + b * sL + I * BI;                  // rows I*BI.., column k
-  const double* K = Kt + b * sK + (long long)C * BC * ldk;   // column c, rows k
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
+  const double* L = Linv + b * sL + I * BI + 2 * lane;                 // + k*ld per row
+  const double* K = Kt2 + b * sK + ((long long)C * BC) * 2 + 2 * lane; // + (kp*mc)*2 (+128)
+  const int nsteps = (I + 1) * (BI / BK);
 
-  __shared__ double As[BK * PA];
-  __shared__ double Bs[BC * PB];
-  __shared__ double red[2][2][BC];
+  auto issue = [&](int s, double* st) {
+    const int k0 = s * BK;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {              // A rows k0 + 4w + r
+      const int kr = 4 * w + r;
+      glds16(L + (long long)(k0 + kr) * ld, st + kr * APITCH);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {              // B: k-pair 2w + (r >> 1), half r & 1
+      const int kpl = 2 * w + (r >> 1), h = r & 1;
+      glds16(K + ((long long)(k0 / 2 + kpl) * mc) * 2 + h * 128,
+             st + ASTAGE + kpl * 256 + h * 128);
+    }
+  };
 
   f64x4 acc[4][4];
 #pragma unroll
@@ -62,53 +136,34 @@ __global__ __launch_bounds__(256) void trmm_reduce_kernel(
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[a][c] = zero4();
 
-  // register staging: A = 16 x 128 (i fast), B = 128 cols x 16 k (k fast); 8 doubles each.
-  double2 ra[4], rb[4];
-  const int kend = (I + 1) * BI;
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int g = tid + 256 * q;           // 1024 double2 per operand
-      const int i2 = (g & 63) * 2, ka = g >> 6;
-      ra[q] = *reinterpret_cast<const double2*>(L + i2 + (long long)(k0 + ka) * ld);
-      const int kb = (g & 7) * 2, c = g >> 3;
-      rb[q] = *reinterpret_cast<const double2*>(K + k0 + kb + (long long)c * ldk);
-    }
-  };
-  auto lstore = [&]() {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int g = tid + 256 * q;
-      const int i2 = (g & 63) * 2, ka = g >> 6;
-      *reinterpret_cast<double2*>(&As[ka * PA + i2]) = ra[q];
-      const int kb = (g & 7) * 2, c = g >> 3;
-      Bs[c * PB + kb] = rb[q].x;
-      Bs[c * PB + kb + 1] = rb[q].y;
-    }
-  };
-
-  gload(0);
-  for (int k0 = 0; k0 < kend; k0 += BK) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (k0 + BK < kend) gload(k0 + BK);
+  issue(0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    double* cur = smem + (s & 1) * STAGE;
+    if (s + 1 < nsteps) issue(s + 1, smem + ((s + 1) & 1) * STAGE);
+    const double* As = cur;
+    const double* Bs = cur + ASTAGE;
 #pragma unroll
     for (int k4 = 0; k4 < BK / 4; ++k4) {
       const int k = k4 * 4 + lk;
       double a[4], bb[4];
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = As[k * PA + wr * 64 + mi * 16 + li];
+      for (int mi = 0; mi < 4; ++mi) a[mi] = As[k * APITCH + wr * 64 + mi * 16 + li];
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) bb[nj] = Bs[(wc * 64 + nj * 16 + li) * PB + k];
+      for (int nj = 0; nj < 4; ++nj)
+        bb[nj] = Bs[((k >> 1) * BC + wc * 64 + nj * 16 + li) * 2 + (k & 1)];
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = mfma16x16x4(a[mi], bb[nj], acc[mi][nj]);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
   // epilogue: column partial sums of V*z and V^2 over this tile's 128 rows
+  double* red = smem;   // [2 wr][2 kind][BC]; the loop's last barrier retired all LDS reads
   const double* zb = z + (long long)b * npad + I * BI + wr * 64;
   double zr[4][4];
 #pragma unroll
@@ -131,8 +186,8 @@ __global__ __launch_bounds__(256) void trmm_reduce_kernel(
     sm += __shfl_xor(sm, 32, 64);
     sv += __shfl_xor(sv, 32, 64);
     if (lk == 0) {
-      red[wr][0][wc * 64 + nj * 16 + li] = sm;
-      red[wr][1][wc * 64 + nj * 16 + li] = sv;
+      red[(wr * 2 + 0) * BC + wc * 64 + nj * 16 + li] = sm;
+      red[(wr * 2 + 1) * BC + wc * 64 + nj * 16 + li] = sv;
     }
   }
   __syncthreads();
@@ -140,8 +195,8 @@ __global__ __launch_bounds__(256) void trmm_reduce_kernel(
     const int col = C * BC + tid;
     double* pm = part + ((long long)(b * 2 + 0) * NI + I) * mc;
     double* pv = part + ((long long)(b * 2 + 1) * NI + I) * mc;
-    pm[col] = red[0][0][tid] + red[1][0][tid];
-    pv[col] = red[0][1][tid] + red[1][1][tid];
+    pm[col] = red[0 * BC + tid] + red[2 * BC + tid];
+    pv[col] = red[1 * BC + tid] + red[3 * BC + tid];
   }
 }
 
@@ -163,6 +218,30 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
   }
   mean[(long long)b * ldo + c0 + j] = sm;
   var[(long long)b * ldo + c0 + j] = s_pred[b] - sv;
+}
+
+template <int D>
+hipError_t cross_kp_launch_d(const double* X, int n, int ldx, const double* Xs, int mv,
+                             int ldxs, int d, const double* beta, int ldbeta, const double* s,
+                             double* Kt2, int mc, int npad, long long sK, int batch,
+                             hipStream_t st) {
+  dim3 grid(gp_ceil_div(mc, 256), npad / 64, batch);
+  hipLaunchKernelGGL((cross_kp_kernel<D>), grid, dim3(256), 0, st, X, n, ldx, Xs, mv, ldxs, d,
+                     beta, ldbeta, s, Kt2, mc, sK);
+  return hipGetLastError();
+}
+
+hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, int mv, int ldxs,
+                           int d, const double* beta, int ldbeta, const double* s, double* Kt2,
+                           int mc, int npad, long long sK, int batch, hipStream_t st) {
+  if (d <= 8)
+    return cross_kp_launch_d<8>(X, n, ldx, Xs, mv, ldxs, d, beta, ldbeta, s, Kt2, mc, npad, sK,
+                                batch, st);
+  if (d <= 16)
+    return cross_kp_launch_d<16>(X, n, ldx, Xs, mv, ldxs, d, beta, ldbeta, s, Kt2, mc, npad, sK,
+                                 batch, st);
+  return cross_kp_launch_d<32>(X, n, ldx, Xs, mv, ldxs, d, beta, ldbeta, s, Kt2, mc, npad, sK,
+                               batch, st);
 }
 
 struct Plan {
@@ -250,14 +329,14 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
     const int c0 = ch * p.mc;
     const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
     gpfit_prof_begin(GP_PROF_CROSS, stream);
-    GP_CK(gpfit_ardse_launch(X, n, ldx, Xs + (long long)c0 * ldxs, mv, ldxs, d, beta, ldbeta,
-                             s, nullptr, kt, p.npad, sK, p.npad, p.mc, batch, stream));
+    GP_CK(cross_kp_launch(X, n, ldx, Xs + (long long)c0 * ldxs, mv, ldxs, d, beta, ldbeta, s,
+                          kt, p.mc, p.npad, sK, batch, stream));
     gpfit_prof_end(GP_PROF_CROSS, stream);
     const int ncol_tiles = gp_ceil_div(mv, BC);
     gpfit_prof_begin(GP_PROF_TRMM, stream);
     hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0,
-                       stream, Linv, ldinv, strideInv, kt, p.npad, sK, z, p.npad, part, p.NI,
-                       ncol_tiles, p.mc);
+                       stream, Linv, ldinv, strideInv, kt, p.mc, sK, z, p.npad, part, p.NI,
+                       ncol_tiles);
     gpfit_prof_end(GP_PROF_TRMM, stream);
     GP_CK(hipGetLastError());
     hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0,
