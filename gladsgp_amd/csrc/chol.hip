@@ -15,12 +15,19 @@
 // own update (diag_factor_inv below), so each step is two launches (panel, update+diag) and the
 // serial diagonal work overlaps the rest of the trailing update.
 //
-// diag_factor_inv: one 256-thread block, register resident (see the function for the scheme):
-// X = L^-1 comes out of the same right-looking sweep as L (X_j. = R_j. / L_jj,
-// R_i. -= L_ij X_j.), one barrier and 32 FMAs per thread per column step.
+// diag_factor_inv: 4 waves, register resident (see the function for the scheme): X = L^-1
+// comes out of the same right-looking sweep as L (X_j. = R_j. / L_jj, R_i. -= L_ij X_j.),
+// one barrier and 16 FMAs per thread per column step.
 #include "gpfit_common.h"
 #include "gpfit_profile.h"
 #include "../../include/gpfit.h"
+
+#ifdef GPFIT_DIAG_STAMPS
+__device__ unsigned long long gpfit_diag_stamps[16];
+extern "C" int gp_diag_stamps(unsigned long long* host16) {
+  return (int)hipMemcpyFromSymbol(host16, HIP_SYMBOL(gpfit_diag_stamps), 16 * 8);
+}
+#endif
 
 namespace {
 
@@ -30,12 +37,12 @@ constexpr int LP = NB + 1;  // LDS pitch (doubles)
 struct __align__(16) Smem {
   double As[NB * LP];
   double Bs[NB * LP];
-  double VA[2][NB];    // scaled L column of the current step (zeros at and above the pivot)
-  double RR[2][NB];    // unscaled R row of the current step
+  double VA[2][NB];    // step vector V (L column below the pivot, R row at and left of it)
   double sps[NB];      // L_jj
   double invs[NB];     // 1 / L_jj
   double inv[2];
   double red[4];
+  int bad[NB];         // per-column non-PD pivot flags (written once, scanned at the end)
   int fail;
 };
 
@@ -112,116 +119,122 @@ GP_DEV void store_tile(double* Cs, const f64x4 (&acc)[2][2], double* __restrict_
   }
 }
 
-// Factor + invert the 64x64 tile held (full, symmetric) in T[row * LP + col]; nb valid rows
-// (rows/cols >= nb are identity padding).  On return T holds L (lower) and U holds L^-1
-// (lower, zero upper); returns 0 or the 1-based local index of the first non-PD pivot.
+// Factor + invert the 64x64 tile held (full, symmetric) in T[row * LP + col]; all 256 threads
+// call it.  nb valid rows (rows/cols >= nb are identity padding).  On return T holds L (lower,
+// zero upper), U holds L^-1 (lower, zero upper); returns 0 or the 1-based local index of the
+// first non-PD pivot.
 //
-// Thread t owns row i = t & 63 and the 16 contiguous columns c = 16 cq + u (cq = t >> 6,
-// wave-uniform) of A and of R (R starts as I).  Step j needs only
-//   VA[c] = L[c][j] = A[c][j] / L[j][j]  (zero for c <= j)   and   RR[c] = R[j][c] (zero c > j)
-// so the update is 32 unconditional FMAs per thread:
-//   A[i][c] -= L[i][j] VA[c],   R[i][c] -= (L[i][j] / L[j][j]) RR[c]
-// (finalised L columns / R entries see zeros and stay put; X = L^-1 rows are R rows / L_ii and
-// the L columns are kept unscaled until the end).  The wave owning column j+1 computes the next
-// pivot from its own registers and publishes VA for step j+1; lane j+1 of every wave publishes
-// its slice of R row j+1 — one barrier per step, ping-pong buffers, no selects in the loop.
+// Thread (row i = t & 63, wave cq = t >> 6) owns the 16 register slots w[u] of columns
+// c = 16 cq + u.  Slot c holds A[i][c] until column c is factored and R[i][c] afterwards
+// (R starts as I; X = L^-1 has rows R_i. / L_ii), so step j is one update per slot:
+//   w[c] -= L[i][j] * V[c]              for c > j,  V[c] = L[c][j]
+//   w[c] -= (L[i][j] / L_jj) * V[c]     for c <= j, V[c] = R[j][c] (unscaled, V[j] = 1)
+// The two halves of V come from disjoint writers (the wave owning column j: lanes c > j;
+// lane j of every wave: its slots c <= j), so V is one LDS vector, ping-ponged, and a step is
+// one barrier + 16 FMAs per thread.  The j loop is unrolled by 16 so the owner wave and slot
+// of column j are compile-time; there is no early exit (a failure is flagged, the sweep
+// finishes on garbage that is discarded) so the unroll always happens.
 GP_DEV int diag_factor_inv(Smem& sm, double* T, double* U, int nb, double* ld_out) {
   const int tid = threadIdx.x;
   const int i = tid & (NB - 1);
   const int cq = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cb = cq * 16;
-  double a[16], r[16];
+  double w[16];
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    a[u] = T[i * LP + cb + u];
-    r[u] = (cb + u == i) ? 1.0 : 0.0;
-  }
-  // publish step 0: column 0 is owned by wave 0 (u = 0), row 0 of R = e_0
-  if (tid == 0) sm.fail = 0;
-  if (cq == 0) {
-    const double piv = readlane_f64(a[0], 0);
-    const bool bad = !(piv > 0.0) || !isfinite(piv);
-    const double inv = rsqrt_nr(piv), sp = piv * inv;
-    sm.VA[0][i] = (i > 0) ? a[0] * inv : 0.0;
-    if (i == 0) {
-      sm.inv[0] = inv;
-      sm.sps[0] = sp;
-      sm.invs[0] = inv;
-      if (bad) sm.fail = 1;
+  for (int u = 0; u < 16; ++u) w[u] = T[i * LP + cb + u];
+
+  // publish step j's V / pivot (owner wave of column j, slot uj, pivot already computed by
+  // every wave from its own slot uj: only the owner's copy is the real one) and the R row
+  auto publish = [&](int j, int own, int uj, int q, double piv, double inv) {
+    if (cq == own) {
+      if (i > j) {
+        const double l = w[uj] * inv;                // L[i][j]
+        sm.VA[q][i] = l;
+        T[i * LP + j] = l;                           // T's column j was read only by this wave
+      }
+      w[uj] = (i == j) ? 1.0 : 0.0;                  // slot j now holds R[i][j] (= delta_ij)
+      if (i == 0) {
+        sm.inv[q] = inv;
+        sm.invs[j] = inv;
+        sm.sps[j] = piv * inv;
+        sm.bad[j] = (!(piv > 0.0) || !isfinite(piv)) ? 1 : 0;
+      }
     }
-  }
-  if (i == 0) {
+    // R[j][c] for c <= j (V[j] = 1): all 16 slots of waves left of the owner, slots u <= uj
+    // of the owner (uj is compile-time) — two uniform cases, no per-slot branches
+    if (i == j) {
+      if (cq < own) {
 #pragma unroll
-    for (int u = 0; u < 16; u += 2) {
-      double2 y;
-      y.x = r[u];
-      y.y = r[u + 1];
-      *reinterpret_cast<double2*>(&sm.RR[0][cb + u]) = y;
+        for (int u = 0; u < 16; u += 2) {
+          double2 y;
+          y.x = w[u];
+          y.y = w[u + 1];
+          *reinterpret_cast<double2*>(&sm.VA[q][cb + u]) = y;
+        }
+      } else if (cq == own) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (u <= uj) sm.VA[q][cb + u] = w[u];
+      }
     }
+  };
+
+  {
+    const double piv = readlane_f64(w[0], 0);
+    publish(0, 0, 0, 0, piv, rsqrt_nr(piv));
   }
-  bool stop = false;
 #pragma unroll 1
-  for (int jb = 0; jb < NB / 16 && !stop; ++jb) {
+  for (int jb = 0; jb < NB / 16; ++jb) {
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {
       const int j = jb * 16 + jj;
-      const int p = jj & 1, q = p ^ 1;
+      const int p = jj & 1;
       __syncthreads();
-      if (sm.fail) { stop = true; break; }
       const double inv = sm.inv[p];
-      const double lij = sm.VA[p][i];
-      const double l2 = lij * inv;
+      const double vi = sm.VA[p][i];
+      const double m1 = (i > j) ? vi : 0.0;          // L[i][j]
+      const double m2 = m1 * inv;                    // L[i][j] / L_jj
+      double v[16];
 #pragma unroll
       for (int u = 0; u < 16; u += 2) {
-        const double2 va = *reinterpret_cast<const double2*>(&sm.VA[p][cb + u]);
-        const double2 rr = *reinterpret_cast<const double2*>(&sm.RR[p][cb + u]);
-        a[u] = fma(-lij, va.x, a[u]);
-        a[u + 1] = fma(-lij, va.y, a[u + 1]);
-        r[u] = fma(-l2, rr.x, r[u]);
-        r[u + 1] = fma(-l2, rr.y, r[u + 1]);
+        const double2 x = *reinterpret_cast<const double2*>(&sm.VA[p][cb + u]);
+        v[u] = x.x;
+        v[u + 1] = x.y;
       }
+      // slot u1 first in every wave: in the owner of column j+1 it carries the next pivot, whose
+      // readlane -> rsqrt chain then overlaps the other 15 FMAs (straight-line code)
+      const int own1 = (jj < 15) ? jb : jb + 1, u1 = (jj + 1) & 15;
+      w[u1] = fma(-((cb + u1 > j) ? m1 : m2), v[u1], w[u1]);
+      double piv1 = 0.0, inv1 = 0.0;
       if (j + 1 < NB) {
-        // column j+1: owner wave and register slot are compile-time per jj.  The pivot chain
-        // (readlane -> rsqrt -> publish) is the step's critical path; it is straight-line code
-        // in every wave, only the owner's stores are predicated.
-        const int own = (jj < 15) ? jb : jb + 1;
-        const int uo = (jj + 1) & 15;
-        const double piv = readlane_f64(a[uo], j + 1);
-        const double inv1 = rsqrt_nr(piv), sp = piv * inv1;
-        if (cq == own) {
-          const bool bad = !(piv > 0.0) || !isfinite(piv);
-          sm.VA[q][i] = (i > j + 1) ? a[uo] * inv1 : 0.0;
-          if (i == 0) {
-            sm.inv[q] = inv1;
-            sm.sps[j + 1] = sp;
-            sm.invs[j + 1] = inv1;
-            if (bad) sm.fail = j + 2;
-          }
-        }
-        if (i == j + 1) {
-#pragma unroll
-          for (int u = 0; u < 16; u += 2) {
-            double2 y;
-            y.x = r[u];
-            y.y = r[u + 1];
-            *reinterpret_cast<double2*>(&sm.RR[q][cb + u]) = y;
-          }
-        }
+        piv1 = readlane_f64(w[u1], j + 1);
+        inv1 = rsqrt_nr(piv1);
       }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if (u == u1) continue;
+        const int c = cb + u;
+        w[u] = fma(-((c > j) ? m1 : m2), v[u], w[u]);
+      }
+      if (j + 1 < NB) publish(j + 1, own1, u1, p ^ 1, piv1, inv1);
     }
   }
   __syncthreads();
-  const int f = sm.fail;
-  if (f) return (f <= nb) ? f : 0;
+  if (tid < 64) {
+    const unsigned long long badm = __ballot(sm.bad[tid] != 0 && tid < nb);
+    if (tid == 0) sm.fail = badm ? (__ffsll((long long)badm)) : 0;
+  }
+  __syncthreads();
+  const int f = sm.fail;              // first bad pivot among the nb valid columns
+  if (f) return f;
   const double inv_i = sm.invs[i];
-  double lg = 0.0;
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int c = cb + u;
-    T[i * LP + c] = (c < i) ? a[u] * sm.invs[c] : ((c == i) ? sm.sps[i] : 0.0);
-    U[i * LP + c] = (c <= i) ? r[u] * inv_i : 0.0;
+    U[i * LP + c] = (c <= i) ? w[u] * inv_i : 0.0;
+    if (c >= i) T[i * LP + c] = (c == i) ? sm.sps[i] : 0.0;   // c < i: written by publish
   }
-  if (cq == 0 && i < nb) lg = 2.0 * log(sm.sps[i]);
+  double lg = (cq == 0 && i < nb) ? 2.0 * log(sm.sps[i]) : 0.0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
   if ((tid & 63) == 0) sm.red[tid >> 6] = lg;
