@@ -40,6 +40,18 @@ SIGNATURES = {
                         c_void_p]),
     "gp_nll": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p,
                        c_void_p, c_int, c_void_p]),
+    "gp_dgemm_ws_bytes": (c_ll, [c_int, c_int, c_int]),
+    "gp_dgemm": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.c_double, c_void_p, c_int,
+                         c_void_p, c_int, ctypes.c_double, c_void_p, c_int, c_void_p, c_ll,
+                         c_void_p]),
+    "gp_sim_stats": (c_int, [c_void_p, c_int, c_int, c_ll, ctypes.c_double, c_void_p, c_void_p,
+                             c_void_p]),
+    "gp_standardize": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_ll,
+                               c_int, c_void_p]),
+    "gp_shift_diag": (c_int, [c_void_p, c_int, c_int, ctypes.c_double, c_void_p]),
+    "gp_rowscale": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "gp_syevj": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                         ctypes.c_double, c_void_p, c_int, c_void_p]),
     "gp_profile_enable": (c_int, [c_int]),
     "gp_profile_reset": (c_int, []),
     "gp_profile_read": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),

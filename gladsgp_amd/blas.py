@@ -1,0 +1,126 @@
+"""Column-major fp64 dense helpers over libgpfit (GEMM, statistics, eigensolver).
+
+A column-major (rows x cols) matrix is a torch tensor ``t`` of shape (cols, ld) with element
+(i, j) at ``t[j, i]`` — i.e. the row-major view of its transpose.  :class:`CM` carries the
+logical shape and leading dimension so the GEMM call reads like BLAS.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _capi
+from .kernels import F64, _stream
+
+
+@dataclass
+class CM:
+    """Column-major view: logical ``rows x cols`` with leading dimension ``ld``."""
+
+    t: torch.Tensor
+    rows: int
+    cols: int
+    ld: int
+
+    @staticmethod
+    def empty(rows: int, cols: int, device) -> "CM":
+        t = torch.empty((max(cols, 1), max(rows, 1)), dtype=F64, device=device)
+        return CM(t, rows, cols, max(rows, 1))
+
+    @staticmethod
+    def of_rowmajor(a: torch.Tensor) -> "CM":
+        """A C-order (r x c) tensor seen column-major is its transpose: (c x r), ld = c."""
+        a = a.contiguous()
+        r, c = a.shape
+        return CM(a, c, r, c)
+
+    def rowmajor_T(self) -> torch.Tensor:
+        """The logical matrix transposed, as a C-order torch tensor (cols x rows) view."""
+        return self.t[: self.cols, : self.rows]
+
+    def logical(self) -> torch.Tensor:
+        return self.rowmajor_T().transpose(0, 1)
+
+    def ptr(self) -> int:
+        return self.t.data_ptr()
+
+
+_WS: dict = {}
+
+
+def _ws(nbytes: int, device) -> torch.Tensor | None:
+    if nbytes <= 0:
+        return None
+    key = str(device)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def gemm(transa: bool, transb: bool, A: CM, B: CM, alpha: float = 1.0, beta: float = 0.0,
+         C: CM | None = None) -> CM:
+    """C = alpha op(A) op(B) + beta C on MFMA (split-K for long inner dimensions)."""
+    m = A.cols if transa else A.rows
+    k = A.rows if transa else A.cols
+    kb = B.cols if transb else B.rows
+    n = B.rows if transb else B.cols
+    if k != kb:
+        raise ValueError(f"gemm: inner dimensions differ ({k} vs {kb})")
+    dev = A.t.device
+    if C is None:
+        C = CM.empty(m, n, dev)
+        beta = 0.0
+    lib = _capi.lib()
+    nbytes = lib.gp_dgemm_ws_bytes(m, n, k)
+    ws = _ws(nbytes, dev)
+    _capi.call("gp_dgemm", int(transa), int(transb), m, n, k, float(alpha), A.ptr(), A.ld,
+               B.ptr(), B.ld, float(beta), C.ptr(), C.ld,
+               ws.data_ptr() if ws is not None else None, nbytes if ws is not None else 0,
+               _stream(dev))
+    return C
+
+
+def sim_stats(Y: torch.Tensor, sd_floor: float = 1e-6):
+    """mu, sd(ddof=1, floored) over rows of a C-order (n x ny) ensemble (src/model.py:60-64)."""
+    Y = Y.contiguous()
+    n, ny = Y.shape
+    mu = torch.empty(ny, dtype=F64, device=Y.device)
+    sd = torch.empty(ny, dtype=F64, device=Y.device)
+    _capi.call("gp_sim_stats", Y.data_ptr(), n, ny, ny, float(sd_floor), mu.data_ptr(),
+               sd.data_ptr(), _stream(Y.device))
+    return mu, sd
+
+
+def standardize(Y: torch.Tensor, mu: torch.Tensor, sd: torch.Tensor, inverse: bool = False,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """(Y - mu)/sd, or Y sd + mu when ``inverse`` (C-order rows x ny)."""
+    Y = Y.contiguous()
+    n, ny = Y.shape
+    out = torch.empty_like(Y) if out is None else out
+    _capi.call("gp_standardize", Y.data_ptr(), n, ny, ny, mu.data_ptr(), sd.data_ptr(),
+               out.data_ptr(), out.stride(0), int(inverse), _stream(Y.device))
+    return out
+
+
+def shift_diag(G: CM, factor: float) -> None:
+    _capi.call("gp_shift_diag", G.ptr(), G.rows, G.ld, float(factor), _stream(G.t.device))
+
+
+def rowscale(M: CM, f: torch.Tensor, inverse: bool = False) -> None:
+    _capi.call("gp_rowscale", M.ptr(), M.rows, M.cols, M.ld, f.data_ptr(), int(inverse),
+               _stream(M.t.device))
+
+
+def syevj(A: CM, max_sweeps: int = 30, tol: float = 1e-15, want_sqrt: bool = False):
+    """Eigen-decomposition of a symmetric r x r matrix (destroyed): (W desc, V, sweeps)."""
+    r = A.rows
+    dev = A.t.device
+    W = torch.empty(r, dtype=F64, device=dev)
+    V = CM.empty(r, r, dev)
+    sweeps = torch.zeros(1, dtype=torch.int32, device=dev)
+    _capi.call("gp_syevj", A.ptr(), r, A.ld, W.data_ptr(), V.ptr(), V.ld, int(max_sweeps),
+               float(tol), sweeps.data_ptr(), int(want_sqrt), _stream(dev))
+    return W, V, sweeps

@@ -1,0 +1,286 @@
+// Fit-side dense kernels (fp64): general MFMA GEMM with split-K, column statistics and
+// elementwise standardisation.  They implement the non-GP arithmetic of the drop-in surface:
+//   src/svd.py:52-64   Y = X Omega, (X X^T) Y, Q^T X, U = Q U_B      (randomized SVD, A2)
+//   src/model.py:60-72 mu = mean(Y, 0), sd = std(Y, ddof=1, 0) floored, Y_std      (A1)
+//   src/model.py:101, 219-223  K = diag(S) Vh / sqrt(n), w = Y_std pinv(K)           (A3, A4)
+//   SepiaEmulatorPrediction.get_y(): y = (w K) sd + mu                              (A9)
+// GEMM: 64x64 output tiles, 256 threads = 4 waves (2x2 of 32x32, v_mfma_f64_16x16x4_f64),
+// K staged through LDS 64 at a time with operand transposition folded into the staging;
+// split-K over grid.z writes partial slabs that a second kernel reduces deterministically
+// (no atomics), so X X^T with K = 1.35M still fills all 256 CUs.
+#include "gpfit_common.h"
+#include "../../include/gpfit.h"
+
+namespace {
+
+constexpr int TB = 64;
+constexpr int TP = TB + 1;
+
+// S[k][x] = op(M)(x, k) for a 64x64 block at (x0, k0); NAT: M[x + k*ld], TRN: M[k + x*ld].
+template <bool TRN>
+GP_DEV void stage_g(double* S, const double* __restrict__ M, int ld, int x0, int xmax, int k0,
+                    int kmax) {
+#pragma unroll 4
+  for (int q = 0; q < (TB * TB) / 256; ++q) {
+    const int g = threadIdx.x + 256 * q;
+    const int fast = g & (TB - 1), slow = g >> 6;
+    int x, k;
+    if (!TRN) { x = fast; k = slow; } else { k = fast; x = slow; }
+    const int gx = x0 + x, gk = k0 + k;
+    double v = 0.0;
+    if (gx < xmax && gk < kmax)
+      v = TRN ? M[gk + (long long)gx * ld] : M[gx + (long long)gk * ld];
+    S[k * TP + x] = v;
+  }
+}
+
+// opA(i,k): transa=0 -> A[i + k*lda] (NAT staging), 1 -> A[k + i*lda] (TRN staging)
+// opB(k,j): transb=0 -> B[k + j*ldb] (TRN staging), 1 -> B[j + k*ldb] (NAT staging)
+template <int TA, int TBT>
+__global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, int kchunk,
+                                                   const double* __restrict__ A, int lda,
+                                                   const double* __restrict__ B, int ldb,
+                                                   double alpha, double beta,
+                                                   double* __restrict__ C, int ldc,
+                                                   double* __restrict__ part) {
+  __shared__ double As[TB * TP];
+  __shared__ double Bs[TB * TP];
+  const int tilesM = gp_ceil_div(M, TB);
+  const int ti = blockIdx.x % tilesM, tj = blockIdx.x / tilesM;
+  const int i0 = ti * TB, j0 = tj * TB;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = zero4();
+  for (int k0 = kb; k0 < ke; k0 += TB) {
+    stage_g<TA != 0>(As, A, lda, i0, M, k0, ke);
+    stage_g<TBT == 0>(Bs, B, ldb, j0, N, k0, ke);
+    __syncthreads();
+#pragma unroll 4
+    for (int k4 = 0; k4 < TB / 4; ++k4) {
+      const int k = k4 * 4 + lk;
+      const double a0 = As[k * TP + wr * 32 + li], a1 = As[k * TP + wr * 32 + 16 + li];
+      const double b0 = Bs[k * TP + wc * 32 + li], b1 = Bs[k * TP + wc * 32 + 16 + li];
+      acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
+      acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
+      acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
+      acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+  // transpose through LDS for coalesced column-major stores
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + mi * 16 + lk + 4 * r, col = wc * 32 + nj * 16 + li;
+        As[col * TP + row] = acc[mi][nj][r];
+      }
+  __syncthreads();
+  for (int g = threadIdx.x; g < TB * TB; g += 256) {
+    const int row = g & (TB - 1), col = g >> 6;
+    const int gi = i0 + row, gj = j0 + col;
+    if (gi >= M || gj >= N) continue;
+    const double v = As[col * TP + row];
+    if (part) {
+      part[(long long)blockIdx.z * M * N + gi + (long long)gj * M] = v;
+    } else {
+      double* c = C + gi + (long long)gj * ldc;
+      *c = (beta == 0.0) ? alpha * v : fma(alpha, v, beta * *c);
+    }
+  }
+}
+
+__global__ void splitk_reduce_kernel(const double* __restrict__ part, int splits, int M, int N,
+                                     double alpha, double beta, double* __restrict__ C,
+                                     int ldc) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)M * N) return;
+  const int gi = (int)(idx % M), gj = (int)(idx / M);
+  double s = 0.0;
+  for (int p = 0; p < splits; ++p) s += part[(long long)p * M * N + idx];
+  double* c = C + gi + (long long)gj * ldc;
+  *c = (beta == 0.0) ? alpha * s : fma(alpha, s, beta * *c);
+}
+
+int choose_splits(int M, int N, int K) {
+  const int tiles = gp_ceil_div(M, TB) * gp_ceil_div(N, TB);
+  int s = 1;
+  while (tiles * s < 512 && K / (s * 2) >= 256) s *= 2;
+  return s;
+}
+
+// Per-location statistics over simulations of a C-order ensemble Y (n sims x ny locations,
+// row stride ldy) — src/model.py:60-64: mu = mean(Y, 0), sd = std(Y, ddof=1, 0) floored at
+// sd_floor.  Thread per location: each sweep over the n rows reads 256 consecutive locations
+// per block row (coalesced); two passes (mean, then centred sum of squares) as numpy does.
+__global__ __launch_bounds__(256) void simstats_kernel(const double* __restrict__ Y, int n,
+                                                       int ny, long long ldy, double sd_floor,
+                                                       double* __restrict__ mu,
+                                                       double* __restrict__ sd) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= ny) return;
+  double s = 0.0;
+  for (int r = 0; r < n; ++r) s += Y[(long long)r * ldy + c];
+  const double mean = s / n;
+  double q = 0.0;
+  for (int r = 0; r < n; ++r) {
+    const double t = Y[(long long)r * ldy + c] - mean;
+    q = fma(t, t, q);
+  }
+  double v = sqrt(q / (n > 1 ? n - 1 : 1));
+  if (v < sd_floor) v = sd_floor;
+  mu[c] = mean;
+  sd[c] = v;
+}
+
+// out[r*ldo + c] = (Y[r*ldy + c] - mu[c]) / sd[c]   (inverse = 0, src/model.py:72)
+// out[r*ldo + c] =  Y[r*ldy + c] * sd[c] + mu[c]    (inverse = 1, get_y's back-transform)
+__global__ void standardize_kernel(const double* __restrict__ Y, int n, int ny, long long ldy,
+                                   const double* __restrict__ mu, const double* __restrict__ sd,
+                                   double* __restrict__ out, long long ldo, int inverse) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)n * ny) return;
+  const int r = (int)(idx / ny), c = (int)(idx % ny);
+  const double y = Y[(long long)r * ldy + c];
+  out[(long long)r * ldo + c] = inverse ? fma(y, sd[c], mu[c]) : (y - mu[c]) / sd[c];
+}
+
+// A[i][i] += factor * trace(A) — the shift of shifted CholeskyQR (one block).
+__global__ __launch_bounds__(256) void shift_diag_kernel(double* __restrict__ A, int r, int lda,
+                                                         double factor) {
+  __shared__ double red[4];
+  double t = 0.0;
+  for (int i = threadIdx.x; i < r; i += 256) t += A[i + (long long)i * lda];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  const double tr = (red[0] + red[1]) + (red[2] + red[3]);
+  for (int i = threadIdx.x; i < r; i += 256) A[i + (long long)i * lda] += factor * tr;
+}
+
+// scale row i of a column-major (rows x cols) matrix by f[i] (or 1/f[i] when inv=1, 0 if f=0)
+__global__ void rowscale_kernel(double* __restrict__ M, int rows, int cols, int ld,
+                                const double* __restrict__ f, int inv) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)rows * cols) return;
+  const int i = (int)(idx % rows), j = (int)(idx / rows);
+  const double fi = f[i];
+  const double g = inv ? (fi != 0.0 ? 1.0 / fi : 0.0) : fi;
+  M[i + (long long)j * ld] *= g;
+}
+
+}  // namespace
+
+extern "C" int gp_shift_diag(double* A, int r, int lda, double factor, hipStream_t stream) {
+  if (!A) return -1;
+  if (r < 0) return -2;
+  if (lda < r || lda < 1) return -3;
+  if (r == 0) return 0;
+  hipLaunchKernelGGL(shift_diag_kernel, dim3(1), dim3(256), 0, stream, A, r, lda, factor);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+extern "C" int gp_rowscale(double* M, int rows, int cols, int ld, const double* f, int inv,
+                           hipStream_t stream) {
+  if (!M) return -1;
+  if (rows < 0) return -2;
+  if (cols < 0) return -3;
+  if (ld < rows || ld < 1) return -4;
+  if (!f) return -5;
+  if (rows == 0 || cols == 0) return 0;
+  const long long tot = (long long)rows * cols;
+  hipLaunchKernelGGL(rowscale_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream,
+                     M, rows, cols, ld, f, inv);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+extern "C" long long gp_dgemm_ws_bytes(int m, int n, int k) {
+  if (m <= 0 || n <= 0 || k <= 0) return 0;
+  const int s = choose_splits(m, n, k);
+  return s > 1 ? (long long)s * m * n * 8 : 0;
+}
+
+extern "C" int gp_dgemm(int transa, int transb, int m, int n, int k, double alpha,
+                        const double* A, int lda, const double* B, int ldb, double beta,
+                        double* C, int ldc, void* ws, long long ws_bytes, hipStream_t stream) {
+  if (transa != 0 && transa != 1) return -1;
+  if (transb != 0 && transb != 1) return -2;
+  if (m < 0) return -3;
+  if (n < 0) return -4;
+  if (k < 0) return -5;
+  if (!A && k > 0) return -7;
+  if (lda < (transa ? k : m) || lda < 1) return -8;
+  if (!B && k > 0) return -9;
+  if (ldb < (transb ? n : k) || ldb < 1) return -10;
+  if (!C) return -12;
+  if (ldc < m || ldc < 1) return -13;
+  if (m == 0 || n == 0) return 0;
+  int splits = (k > 0) ? choose_splits(m, n, k) : 1;
+  if (splits > 1 && (!ws || ws_bytes < (long long)splits * m * n * 8)) splits = 1;
+  const int kchunk = (k > 0) ? gp_ceil_div(gp_ceil_div(k, splits), TB) * TB : TB;
+  splits = (k > 0) ? gp_ceil_div(k, kchunk) : 1;
+  double* part = (splits > 1) ? static_cast<double*>(ws) : nullptr;
+  dim3 grid(gp_ceil_div(m, TB) * gp_ceil_div(n, TB), 1, splits);
+#define GP_GEMM(TA_, TB_)                                                                     \
+  hipLaunchKernelGGL((gemm_kernel<TA_, TB_>), grid, dim3(256), 0, stream, m, n, k, kchunk, A, \
+                     lda, B, ldb, alpha, beta, C, ldc, part)
+  if (transa == 0 && transb == 0) GP_GEMM(0, 0);
+  else if (transa == 0 && transb == 1) GP_GEMM(0, 1);
+  else if (transa == 1 && transb == 0) GP_GEMM(1, 0);
+  else GP_GEMM(1, 1);
+#undef GP_GEMM
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  if (part) {
+    const long long tot = (long long)m * n;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       stream, part, splits, m, n, alpha, beta, C, ldc);
+    e = hipGetLastError();
+    if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  }
+  return 0;
+}
+
+extern "C" int gp_sim_stats(const double* Y, int n, int ny, long long ldy, double sd_floor,
+                            double* mu, double* sd, hipStream_t stream) {
+  if (!Y) return -1;
+  if (n < 1) return -2;
+  if (ny < 0) return -3;
+  if (ldy < ny) return -4;
+  if (!mu) return -6;
+  if (!sd) return -7;
+  if (ny == 0) return 0;
+  hipLaunchKernelGGL(simstats_kernel, dim3(gp_ceil_div(ny, 256)), dim3(256), 0, stream, Y, n, ny,
+                     ldy, sd_floor, mu, sd);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+extern "C" int gp_standardize(const double* Y, int n, int ny, long long ldy, const double* mu,
+                              const double* sd, double* out, long long ldo, int inverse,
+                              hipStream_t stream) {
+  if (!Y) return -1;
+  if (n < 0) return -2;
+  if (ny < 0) return -3;
+  if (ldy < ny) return -4;
+  if (!mu) return -5;
+  if (!sd) return -6;
+  if (!out) return -7;
+  if (ldo < ny) return -8;
+  if (n == 0 || ny == 0) return 0;
+  const long long tot = (long long)n * ny;
+  hipLaunchKernelGGL(standardize_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     stream, Y, n, ny, ldy, mu, sd, out, ldo, inverse);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}

@@ -72,4 +72,4 @@ GP_DEV int xcd_remap(int b, int nwg) {
   return base + pos;
 }
 
-static inline int gp_ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline int gp_ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,101 @@
+"""Randomized fixed-rank SVD on the GPU — drop-in for ``src/svd.py`` (``randomized_svd``).
+
+Reference: ``src/svd.py:12-82`` (Halko et al. 2011): Gaussian test matrix Omega (ny x (p+k),
+float32, drawn from ``np.random``), ``Y = X Omega``, ``q`` power iterations ``Y = X X^T Y``,
+``Q = qr(Y)``, ``B = Q^T X``, ``U_B, S, V = svd(B)``, ``U = Q U_B``, truncation to ``p``.
+
+Build (all arithmetic in libgpfit, fp64):
+  * every product is an MFMA GEMM (``gp_dgemm``; the ny-long inner products use split-K);
+    the power iteration is evaluated as ``X (X^T Y)`` — the same matrix as the reference's
+    left-associated ``(X X^T) Y`` without forming the n x n Gram;
+  * ``qr(Y)`` is shifted CholeskyQR3 (Fukaya et al. 2020): ``Y`` after a power step is very
+    ill-conditioned, so the first pass factors ``Y^T Y + s I`` (s = 11 (n r + r(r+1)) u ||Y||^2,
+    a trace bound), two plain CholeskyQR passes then restore orthogonality to ~u.  The
+    Cholesky + inverse is ``gp_potrf_inv``;
+  * ``svd(B)`` comes from the Jacobi eigendecomposition of ``B B^T`` (``gp_syevj``, r <= 128):
+    ``S = sqrt(eig)``, ``V^T = S^-1 U_B^T B``.
+Singular vectors are unique up to sign (and rotation inside clusters); tests compare signed.
+The reference's ``return_error`` bound is always 0 because ``S`` is truncated before ``S[p]``
+is read (src/svd.py:66-76): mirrored.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import kernels
+from .blas import CM, gemm, rowscale, shift_diag, syevj
+
+_U = 2.0 ** -53
+
+
+def _device(dev) -> torch.device:
+    if dev is not None:
+        return torch.device(dev)
+    if not torch.cuda.is_available():
+        raise RuntimeError("randomized_svd runs on the GPU (libgpfit); no HIP device found")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _chol_qr(Y: CM, shift: bool) -> CM:
+    G = gemm(True, False, Y, Y)                              # r x r  = Y^T Y
+    r = G.rows
+    if shift:
+        shift_diag(G, 11.0 * (Y.rows * r + r * (r + 1)) * _U)
+    ch = kernels.cholesky_inverse(G.t[:r, :r].reshape(1, r, r).contiguous())
+    ch.check()
+    Linv = CM(ch.linv_buf[0], r, r, ch.linv_buf.shape[1])
+    return gemm(False, True, Y, Linv)                        # Y L^-T
+
+
+def orthonormalize(Y: CM) -> CM:
+    """Orthonormal basis of range(Y) (n x r, r <= 128): shifted CholeskyQR3."""
+    Q = _chol_qr(Y, shift=True)
+    Q = _chol_qr(Q, shift=False)
+    return _chol_qr(Q, shift=False)
+
+
+def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=None):
+    """Same signature and return shapes as ``src/svd.py:randomized_svd``.
+
+    ``X`` is (m, n) (numpy or torch); returns ``(U (m, p), S (p,), Vh (p, n))`` as numpy arrays
+    when ``X`` is numpy, torch device tensors otherwise.  ``omega`` overrides the test matrix;
+    by default it is drawn exactly as the reference does (``np.random.normal(size=(n, p+k))``
+    cast to float32), so a seeded ``np.random`` reproduces the reference's Omega.
+    """
+    as_numpy = not torch.is_tensor(X)
+    dev = _device(device if as_numpy else (device or X.device))
+    Xt = torch.as_tensor(np.asarray(X) if as_numpy else X, dtype=torch.float64, device=dev)
+    Xt = Xt.contiguous()
+    m_rows, n_cols = Xt.shape
+    if k is None:
+        k = p
+    r = p + k
+    if r > 128:
+        raise ValueError("randomized_svd: p + k must be <= 128 (Jacobi core)")
+    if omega is None:
+        omega = np.random.normal(size=(n_cols, r)).astype(np.float32)
+    Om = torch.as_tensor(np.asarray(omega) if not torch.is_tensor(omega) else omega,
+                         dtype=torch.float64, device=dev).contiguous()
+    Xc = CM.of_rowmajor(Xt)          # (n_cols x m_rows), ld = n_cols
+    Oc = CM.of_rowmajor(Om)          # (r x n_cols)
+    Y = gemm(True, True, Xc, Oc)     # (m_rows x r) = X Omega
+    for _ in range(q):
+        Z = gemm(False, False, Xc, Y)    # (n_cols x r) = X^T Y
+        Y = gemm(True, False, Xc, Z)     # (m_rows x r) = X X^T Y
+    Q = orthonormalize(Y)
+    B = gemm(True, True, Q, Xc)      # (r x n_cols) = Q^T X
+    G = gemm(False, True, B, B)      # (r x r) = B B^T
+    S, UB, _ = syevj(G, want_sqrt=True)      # singular values of B, descending
+    Vh = gemm(True, False, UB, B)    # U_B^T B
+    rowscale(Vh, S, inverse=True)    # S^-1 U_B^T B
+    U = gemm(False, False, Q, UB)    # (m_rows x r)
+    U_t = U.logical()[:, :p].contiguous()
+    S_t = S[:p].contiguous()
+    Vh_t = Vh.logical()[:p, :].contiguous()
+    out = (U_t, S_t, Vh_t)
+    if as_numpy:
+        out = tuple(t.cpu().numpy() for t in out)
+    if return_error:
+        return out, 0.0
+    return out

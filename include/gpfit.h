@@ -117,6 +117,42 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
            const double* w, int ldw, const double* logdet, double* nll, double* work,
            int batch, hipStream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Fit-side dense kernels (src/model.py init_model and src/svd.py randomized_svd).
+ * ---------------------------------------------------------------------------------------- */
+
+/* C = alpha op(A) op(B) + beta C, column-major fp64 on MFMA; op = transpose when trans = 1.
+ * Large-K products are split over K into `ws` (gp_dgemm_ws_bytes(m, n, k) bytes; with a smaller
+ * or NULL ws the product runs unsplit).  Replaces the numpy GEMMs of src/svd.py:52-64
+ * (X Omega, X X^T Y, Q^T X, Q U) and of src/model.py:101, 219-220. */
+long long gp_dgemm_ws_bytes(int m, int n, int k);
+int gp_dgemm(int transa, int transb, int m, int n, int k, double alpha,
+             const double* A, int lda, const double* B, int ldb, double beta,
+             double* C, int ldc, void* ws, long long ws_bytes, hipStream_t stream);
+
+/* Per-location statistics over simulations of a C-order ensemble Y (n x ny, row stride ldy):
+ * mu = mean over rows, sd = std(ddof=1) floored at sd_floor — src/model.py:60-64. */
+int gp_sim_stats(const double* Y, int n, int ny, long long ldy, double sd_floor,
+                 double* mu, double* sd, hipStream_t stream);
+
+/* out = (Y - mu) / sd (inverse = 0, src/model.py:72) or out = Y sd + mu (inverse = 1, the
+ * back-transform of SepiaEmulatorPrediction.get_y), both C-order n x ny with row strides. */
+int gp_standardize(const double* Y, int n, int ny, long long ldy, const double* mu,
+                   const double* sd, double* out, long long ldo, int inverse,
+                   hipStream_t stream);
+
+/* A[i][i] += factor * trace(A) (shifted CholeskyQR); row i of M scaled by f[i] or 1/f[i]. */
+int gp_shift_diag(double* A, int r, int lda, double factor, hipStream_t stream);
+int gp_rowscale(double* M, int rows, int cols, int ld, const double* f, int inv,
+                hipStream_t stream);
+
+/* Symmetric eigendecomposition A = V diag(W) V^T by cyclic Jacobi (r <= 128, one workgroup),
+ * eigenvalues descending (want_sqrt = 1: W = sqrt(max(eig, 0)), the singular values when
+ * A = B B^T); A is destroyed.  `sweeps` (device int, may be NULL) receives the sweep count.
+ * The r x r core of np.linalg.svd(B) in src/svd.py:63 (via B B^T). */
+int gp_syevj(double* A, int r, int lda, double* W, double* V, int ldv, int max_sweeps,
+             double tol, int* sweeps, int want_sqrt, hipStream_t stream);
+
 /*
  * Optional kernel timing (diagnostics; not part of the reference surface).  When enabled with
  * capacity > 0, instrumented launches record a hipEvent pair on their own stream; after the
