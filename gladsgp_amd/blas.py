@@ -105,6 +105,16 @@ def standardize(Y: torch.Tensor, mu: torch.Tensor, sd: torch.Tensor, inverse: bo
     return out
 
 
+def mean_var(x: torch.Tensor, ddof: int = 0):
+    """(mean, var) of all elements of ``x`` (device scalars tensor of 2)."""
+    x = x.contiguous()
+    out = torch.empty(2, dtype=F64, device=x.device)
+    work = torch.empty(1024, dtype=F64, device=x.device)
+    _capi.call("gp_mean_var", x.data_ptr(), x.numel(), int(ddof), out.data_ptr(),
+               work.data_ptr(), _stream(x.device))
+    return out
+
+
 def shift_diag(G: CM, factor: float) -> None:
     _capi.call("gp_shift_diag", G.ptr(), G.rows, G.ld, float(factor), _stream(G.t.device))
 

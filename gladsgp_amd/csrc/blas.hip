@@ -177,7 +177,59 @@ __global__ void rowscale_kernel(double* __restrict__ M, int rows, int cols, int 
   M[i + (long long)j * ld] *= g;
 }
 
+// Two-pass mean / variance of a long vector: grid-stride partial sums into work[blocks], one
+// block reduces them; the second pass is centred (as numpy's var).
+constexpr int kMVBlocks = 1024;
+__global__ __launch_bounds__(256) void partial_sum_kernel(const double* __restrict__ x,
+                                                          long long N,
+                                                          const double* __restrict__ center,
+                                                          double* __restrict__ work) {
+  __shared__ double red[4];
+  const double c = center ? center[0] : 0.0;
+  double s = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < N;
+       i += (long long)gridDim.x * 256) {
+    const double t = x[i] - c;
+    s += center ? t * t : t;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) work[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void finish_sum_kernel(const double* __restrict__ work,
+                                                         int nb, double scale,
+                                                         double* __restrict__ out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) s += work[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = ((red[0] + red[1]) + (red[2] + red[3])) * scale;
+}
+
 }  // namespace
+
+extern "C" int gp_mean_var(const double* x, long long N, int ddof, double* out, double* work,
+                           hipStream_t stream) {
+  if (!x) return -1;
+  if (N < 1) return -2;
+  if (ddof < 0 || ddof >= N) return -3;
+  if (!out) return -4;
+  if (!work) return -5;
+  const int nb = (int)((N + 255) / 256 < kMVBlocks ? (N + 255) / 256 : kMVBlocks);
+  hipLaunchKernelGGL(partial_sum_kernel, dim3(nb), dim3(256), 0, stream, x, N, nullptr, work);
+  hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(256), 0, stream, work, nb, 1.0 / N, out);
+  hipLaunchKernelGGL(partial_sum_kernel, dim3(nb), dim3(256), 0, stream, x, N, out, work);
+  hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(256), 0, stream, work, nb,
+                     1.0 / (double)(N - ddof), out + 1);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
 
 extern "C" int gp_shift_diag(double* A, int r, int lda, double factor, hipStream_t stream) {
   if (!A) return -1;

@@ -1,0 +1,336 @@
+"""Multivariate GP emulator surface (the SEPIA objects the reference drives), on libgpfit.
+
+Reference usage being replaced (SEPIA fork, un-vendored, ``requirements-cc.txt:55``):
+  * ``SepiaData(t_sim, y_sim, y_ind_sim)`` + ``standardize_y`` + ``create_K_basis(K)``
+    (``src/model.py:57-102``)                              -> :class:`EmulatorData`
+  * ``SepiaModel(data)``, ``.get_samples(numsamples, nburn)``, ``.save_model_info`` /
+    ``.restore_model_info`` (``src/model.py:106, 149, 238``; ``assess_all_models.py:471``)
+                                                           -> :class:`EmulatorModel`
+  * ``SepiaEmulatorPrediction(model=, samples=, t_pred=)`` with ``.w`` (S, m, P) and
+    ``.get_y()`` (S, m, ny) (``time_predictions.py:76-79``, ``sensitivity_indices.py:85-88``,
+    ``assess_all_models.py:489-492``)                      -> :class:`EmulatorPrediction`
+
+The GPMSA sim-only model, per MCMC sample s and principal component j (one independent GP
+each), with betaU (S, (d+1) P) reshaped C-order to (S, d+1, P), row 0 the dummy x
+(``mcmc_diagnostics_advanced.py:57``):
+  Sigma_j = (1/lamUz_j) exp(-sum_k beta_kj (t_ik - t_i'k)^2)
+            + (1/lamWs_j + 1/(lamWOs LamSim_j)) I                       (training block)
+  k*_j    = (1/lamUz_j) exp(-sum_k beta_kj (t*_k - t_ik)^2)              (cross-covariance)
+  mean    = k*_j^T Sigma_j^-1 w_hat_j,  var = 1/lamUz_j [+ 1/lamWs_j] - k*_j^T Sigma_j^-1 k*_j
+``pred_nugget`` selects whether 1/lamWs is part of the predictive prior variance (SEPIA's
+exact choice is not verifiable offline — SURVEY §8c — so it is a flag, default on).
+
+Differences from SEPIA, by design: ``.w`` is the posterior MEAN per (sample, PC) and ``.var``
+the marginal variance (SEPIA returns one joint random draw over the m_b x m_b covariance, which
+does not scale to m = 100k); ``sample_w`` draws marginal realisations.  All arithmetic runs
+in libgpfit (fp64); the (sample, PC) pairs are one batched Gram -> Cholesky/L^-1 -> predict.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import blas, kernels
+from . import dist as gdist
+from .blas import CM, gemm
+
+F64 = torch.float64
+
+
+def _dev(device):
+    if device is not None:
+        return torch.device(device)
+    if not torch.cuda.is_available():
+        raise RuntimeError("the emulator runs on a HIP device (libgpfit); none found")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _np(x):
+    return x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+
+
+class SimData:
+    """Simulation block: design, raw and standardised outputs, PCA basis (SEPIA sim_data)."""
+
+    def __init__(self, t_sim, y_sim, y_ind_sim, device):
+        self.device = device
+        self.t = torch.as_tensor(_np(t_sim), dtype=F64, device=device).contiguous()
+        self.y = torch.as_tensor(_np(y_sim), dtype=F64, device=device).contiguous()
+        self.y_ind = np.asarray(y_ind_sim)
+        self.y_mean = None
+        self.y_sd = None
+        self.y_std = None
+        self.K = None          # (P, ny) basis
+
+    @property
+    def n(self) -> int:
+        return self.t.shape[0]
+
+
+class EmulatorData:
+    """Mirror of the SepiaData pieces src/model.py uses (sim-only, x = dummy)."""
+
+    def __init__(self, t_sim, y_sim, y_ind_sim=None, device=None):
+        device = _dev(device)
+        y_ind_sim = np.linspace(0, 1, np.shape(y_sim)[1]) if y_ind_sim is None else y_ind_sim
+        self.sim_data = SimData(t_sim, y_sim, y_ind_sim, device)
+        self.device = device
+
+    def standardize_y(self, y_mean=None, y_sd=None, sd_threshold=1e-6):
+        """y_std = (y - mu)/sd with mu/sd from the ensemble when not given (model.py:60-73)."""
+        sd_ = self.sim_data
+        if y_mean is None or y_sd is None:
+            mu, sd = blas.sim_stats(sd_.y, sd_threshold)
+        else:
+            mu = torch.as_tensor(_np(y_mean), dtype=F64, device=self.device).contiguous()
+            sd = torch.as_tensor(_np(y_sd), dtype=F64, device=self.device).contiguous()
+        sd_.y_mean, sd_.y_sd = mu, sd
+        sd_.y_std = blas.standardize(sd_.y, mu, sd)
+
+    def create_K_basis(self, K):
+        """Set the PCA basis K (P x ny) — SEPIA create_K_basis (model.py:102)."""
+        self.sim_data.K = torch.as_tensor(_np(K), dtype=F64, device=self.device).contiguous()
+
+
+def pc_weights(data: EmulatorData):
+    """w_hat = y_std pinv(K) (n x P) and LamSim = diag(K K^T) — model.py:219; SEPIA's w.
+
+    pinv(K) = K^T (K K^T)^-1 for a full-row-rank basis: two MFMA GEMMs and the P x P
+    Cholesky inverse (K K^T)^-1 = L^-T L^-1.
+    """
+    sd_ = data.sim_data
+    K = CM.of_rowmajor(sd_.K)             # (ny x P) column-major view of K^T
+    Ys = CM.of_rowmajor(sd_.y_std)        # (ny x n)
+    P = sd_.K.shape[0]
+    KKt = gemm(True, False, K, K)         # (P x P) = K K^T
+    lam = torch.diagonal(KKt.logical()).contiguous().clone()
+    YK = gemm(True, False, Ys, K)         # (n x P) = y_std K^T
+    ch = kernels.cholesky_inverse(KKt.t[:P, :P].reshape(1, P, P).contiguous())
+    ch.check()
+    Linv = CM(ch.linv_buf[0], P, P, ch.linv_buf.shape[1])
+    T = gemm(False, True, YK, Linv)       # (n x P) = y_std K^T L^-T
+    W = gemm(False, False, T, Linv)       # (n x P) = y_std K^T L^-T L^-1
+    return W, lam
+
+
+class EmulatorModel:
+    """Mirror of the SepiaModel surface the reference uses (sim-only)."""
+
+    param_names = ("betaU", "lamUz", "lamWs", "lamWOs")
+
+    def __init__(self, data: EmulatorData):
+        self.data = data
+        sd_ = data.sim_data
+        if sd_.K is None or sd_.y_std is None:
+            raise ValueError("EmulatorModel needs standardised y and a K basis")
+        self.device = data.device
+        self.w_hat_cm, lam = pc_weights(data)          # (n x P) column-major
+        self.LamSim = lam
+        self.n, self.d = sd_.t.shape
+        self.P = sd_.K.shape[0]
+        # GPMSA default starting values (SEPIA's defaults; step sizes 03...ipynb:192-208)
+        self.params = {
+            "betaU": np.full((self.d + 1, self.P), 0.1),
+            "lamUz": np.ones((1, self.P)),
+            "lamWs": np.full((1, self.P), 1000.0),
+            "lamWOs": np.full((1, 1), 1000.0),
+        }
+        self.samples = None
+
+    @property
+    def w_hat(self) -> torch.Tensor:
+        """(n, P) PC weights of the training runs."""
+        return self.w_hat_cm.logical()
+
+    # ---------------------------------------------------------------------------------- I/O
+    def set_samples(self, samples: dict):
+        self.samples = {k: np.asarray(v, dtype=np.float64) for k, v in samples.items()}
+
+    def get_samples(self, numsamples=None, nburn=0):
+        """Posterior samples after ``nburn``, optionally ``numsamples`` evenly spaced."""
+        if self.samples is None:
+            raise ValueError("model has no MCMC samples (restore_model_info or set_samples)")
+        tot = len(self.samples["lamUz"])
+        idx = np.arange(nburn, tot)
+        if numsamples is not None and numsamples < len(idx):
+            idx = idx[np.linspace(0, len(idx) - 1, numsamples).astype(int)]
+        return {k: v[idx] for k, v in self.samples.items()}
+
+    def save_model_info(self, path):
+        """Samples + current parameters as ``path + '.npz'`` (plain arrays, no pickle)."""
+        arrs = {f"samples_{k}": v for k, v in (self.samples or {}).items()}
+        arrs.update({f"param_{k}": v for k, v in self.params.items()})
+        np.savez(path if path.endswith(".npz") else path + ".npz", **arrs)
+
+    def restore_model_info(self, path):
+        f = path if path.endswith(".npz") else path + ".npz"
+        with np.load(f, allow_pickle=False) as z:
+            samples = {k[8:]: z[k] for k in z.files if k.startswith("samples_")}
+            for k in z.files:
+                if k.startswith("param_"):
+                    self.params[k[6:]] = z[k]
+        self.samples = samples or None
+
+    # ------------------------------------------------------------------------- likelihood
+    def log_likelihood(self, params=None) -> float:
+        """Sum over PCs of the Gaussian log-likelihood of w_hat_j (no 2pi term, no priors).
+
+        Building block of SEPIA's logLik for the sim-only model (driven by do_mcmc,
+        src/model.py:234-235): one batched Gram -> Cholesky -> nll over the P GPs.
+        """
+        pr = self.params if params is None else params
+        samples = {k: np.asarray(pr[k]).reshape(1, -1) for k in self.param_names}
+        beta, s, delta, _ = gp_params(samples, _np(self.LamSim), self.d, self.P, False)
+        X = self.data.sim_data.t
+        G = kernels.gram(X, torch.as_tensor(beta[0], device=self.device),
+                         torch.as_tensor(s[0], device=self.device),
+                         torch.as_tensor(delta[0], device=self.device), batch=self.P)
+        ch = kernels.cholesky_inverse(G)
+        ch.check()
+        w = self.w_hat.transpose(0, 1).contiguous()           # (P, n)
+        return -float(kernels.nll(ch, w).sum().item())
+
+
+def gp_params(samples, LamSim, d, P, pred_nugget=True):
+    """Per (sample, PC) kernel parameters: beta (S, P, d), s, delta, s_pred (S, P).
+
+    Parameter marshalling only (host, O(S P d)): the covariance arithmetic is in libgpfit.
+    """
+    bu = np.asarray(samples["betaU"], dtype=np.float64)
+    S = bu.shape[0]
+    beta = bu.reshape(S, d + 1, P)[:, 1:, :].transpose(0, 2, 1).copy()
+    lamUz = np.asarray(samples["lamUz"], dtype=np.float64).reshape(S, P)
+    lamWs = np.asarray(samples["lamWs"], dtype=np.float64).reshape(S, P)
+    lamWOs = np.asarray(samples["lamWOs"], dtype=np.float64).reshape(S, 1)
+    lam = np.asarray(LamSim, dtype=np.float64).reshape(1, P)
+    s = 1.0 / lamUz
+    delta = 1.0 / lamWs + 1.0 / (lamWOs * lam)
+    s_pred = s + (1.0 / lamWs if pred_nugget else 0.0)
+    return beta, s, delta, s_pred
+
+
+def predict_units(X, Xs, w_units, beta_u, s_u, delta_u, sp_u, budget_bytes=2 << 30,
+                  m_chunk=0):
+    """Posterior mean / variance of a list of GPs sharing X and Xs: returns (U, m) x 2.
+
+    Units are processed in groups bounded by ``budget_bytes`` of Gram + L^-1 storage.
+    """
+    dev = X.device
+    U = beta_u.shape[0]
+    n = X.shape[0]
+    m = Xs.shape[0]
+    npad = kernels.padded_n(n)
+    per = 8 * (n * n + npad * npad)
+    g = max(1, int(budget_bytes // per))
+    mean = torch.empty((U, m), dtype=F64, device=dev)
+    var = torch.empty((U, m), dtype=F64, device=dev)
+    ws = kernels.PredictWorkspace()
+    for a in range(0, U, g):
+        b = min(U, a + g)
+        G = kernels.gram(X, beta_u[a:b], s_u[a:b], delta_u[a:b], batch=b - a)
+        ch = kernels.cholesky_inverse(G)
+        ch.check()
+        kernels.predict(ch, X, Xs, beta_u[a:b], s_u[a:b], sp_u[a:b], w_units[a:b],
+                        m_chunk=m_chunk, workspace=ws, out=(mean[a:b], var[a:b]))
+        del G, ch
+    return mean, var
+
+
+class EmulatorPrediction:
+    """Predictions of the P PC-GPs for each posterior sample at ``t_pred`` (m x d).
+
+    ``ctx`` (a :class:`gladsgp_amd.dist.Context`) shards the (sample, PC) units round-robin
+    over ranks; rank 0 receives the gathered (S, m, P) results, other ranks hold ``None``.
+    """
+
+    def __init__(self, model: EmulatorModel = None, samples: dict = None, t_pred=None,
+                 pred_nugget: bool = True, ctx: gdist.Context | None = None,
+                 budget_bytes: int = 2 << 30, m_chunk: int = 0):
+        if model is None or samples is None or t_pred is None:
+            raise ValueError("EmulatorPrediction needs model, samples and t_pred")
+        self.model = model
+        dev = model.device
+        X = model.data.sim_data.t
+        Xs = torch.as_tensor(_np(t_pred), dtype=F64, device=dev).reshape(-1, model.d)
+        Xs = Xs.contiguous()
+        beta, s, delta, sp = gp_params(samples, _np(model.LamSim), model.d, model.P,
+                                       pred_nugget)
+        S, P = s.shape
+        self.S, self.m, self.P = S, Xs.shape[0], P
+        units = [(a, j) for a in range(S) for j in range(P)]
+        rank, world = (ctx.rank, ctx.world) if ctx is not None else (0, 1)
+        mine = gdist.shard_units(len(units), rank, world)
+        w_hat = model.w_hat.transpose(0, 1).contiguous()       # (P, n)
+        if mine:
+            sel_s = np.array([units[u][0] for u in mine])
+            sel_j = np.array([units[u][1] for u in mine])
+            t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=F64, device=dev)  # noqa
+            jj = torch.as_tensor(sel_j, device=dev)
+            mean_l, var_l = predict_units(X, Xs, w_hat[jj].contiguous(),
+                                          t(beta[sel_s, sel_j]), t(s[sel_s, sel_j]),
+                                          t(delta[sel_s, sel_j]), t(sp[sel_s, sel_j]),
+                                          budget_bytes, m_chunk)
+        else:
+            mean_l = torch.empty((0, self.m), dtype=F64, device=dev)
+            var_l = torch.empty((0, self.m), dtype=F64, device=dev)
+        if ctx is not None and ctx.distributed:
+            counts = [len(gdist.shard_units(len(units), r, world)) for r in range(world)]
+            both = torch.stack([mean_l, var_l], dim=1) if mean_l.shape[0] else \
+                torch.empty((0, 2, self.m), dtype=F64, device=dev)
+            allb = gdist.gather_rows(ctx, both, counts)
+            if allb is None:
+                self.w_dev = self.var_dev = None
+                return
+            order = np.concatenate([gdist.shard_units(len(units), r, world)
+                                    for r in range(world)])
+            inv = np.empty_like(order)
+            inv[order] = np.arange(len(order))
+            allb = allb[torch.as_tensor(inv, device=allb.device)]
+            mean_u, var_u = allb[:, 0], allb[:, 1]
+        else:
+            mean_u, var_u = mean_l, var_l
+        # units are (s, j) in s-major order -> (S, P, m) -> (S, m, P)
+        self.w_dev = mean_u.reshape(S, P, self.m).permute(0, 2, 1).contiguous()
+        self.var_dev = var_u.reshape(S, P, self.m).permute(0, 2, 1).contiguous()
+
+    @property
+    def w(self) -> np.ndarray:
+        """(S, m, P) posterior mean PC weights (numpy, as the reference consumes ``.w``)."""
+        return None if self.w_dev is None else self.w_dev.cpu().numpy()
+
+    @property
+    def var(self) -> np.ndarray:
+        return None if self.var_dev is None else self.var_dev.cpu().numpy()
+
+    def get_mu_sigma(self):
+        return self.w, self.var
+
+    def sample_w(self, rng=None) -> np.ndarray:
+        """One marginal realisation per (sample, point, PC): mean + sqrt(var) N(0, 1)."""
+        rng = np.random.default_rng() if rng is None else rng
+        z = rng.standard_normal(self.w.shape)
+        return self.w + np.sqrt(np.maximum(self.var, 0.0)) * z
+
+    def get_y(self, std: bool = False, w=None) -> np.ndarray:
+        """Field reconstruction y = (w K) sd + mu, shape (S, m, ny) — SEPIA get_y()."""
+        sd_ = self.model.data.sim_data
+        wd = self.w_dev if w is None else torch.as_tensor(w, dtype=F64,
+                                                            device=self.model.device)
+        S, m, P = wd.shape
+        Wc = CM.of_rowmajor(wd.reshape(S * m, P).contiguous())   # (P x S m)
+        Kc = CM.of_rowmajor(sd_.K)                               # (ny x P)
+        Yc = gemm(False, False, Kc, Wc)                          # (ny x S m) = (w K)^T
+        y = Yc.t[: S * m, : sd_.K.shape[1]]                      # (S m, ny) row-major
+        if not std:
+            y = blas.standardize(y.contiguous(), sd_.y_mean, sd_.y_sd, inverse=True)
+        return y.reshape(S, m, -1).cpu().numpy()
+
+
+# SEPIA-compatible alias for drop-in call sites
+SepiaEmulatorPrediction = EmulatorPrediction
+
+
+def default_data_dir():
+    return os.path.join(os.getcwd(), "data")

@@ -141,6 +141,11 @@ int gp_standardize(const double* Y, int n, int ny, long long ldy, const double* 
                    const double* sd, double* out, long long ldo, int inverse,
                    hipStream_t stream);
 
+/* out[0] = mean(x), out[1] = var(x, ddof) of a length-N vector (two-pass, deterministic);
+ * work holds 1024 doubles.  np.var of the PC truncation residual, src/model.py:222. */
+int gp_mean_var(const double* x, long long N, int ddof, double* out, double* work,
+                hipStream_t stream);
+
 /* A[i][i] += factor * trace(A) (shifted CholeskyQR); row i of M scaled by f[i] or 1/f[i]. */
 int gp_shift_diag(double* A, int r, int lda, double factor, hipStream_t stream);
 int gp_rowscale(double* M, int rows, int cols, int ld, const double* f, int inv,
