@@ -17,6 +17,7 @@
 //   3. finalize           mean = sum_I pm, var = s_pred - sum_I pv
 // z = X w is a small lower-triangular gemv (linalg.hip trmv_kernel).
 #include "gpfit_common.h"
+#include <cstdlib>
 #include "gpfit_profile.h"
 #include "../../include/gpfit.h"
 
@@ -34,7 +35,8 @@ namespace {
 constexpr int BI = 128;   // V tile rows (L^-1 rows)
 constexpr int BC = 128;   // V tile cols (test points)
 constexpr int BK = 16;    // K step
-constexpr long long kDefaultChunkElems = 16ll << 20;   // ~128 MB of Kt per chunk (MALL-sized)
+constexpr long long kDefaultChunkElems = 256ll << 20;  // <= 2 GB of Kt per chunk
+constexpr int kDefaultChunk = 4096;                   // test points per chunk
 
 // Cross-covariance chunk in the k-pair-interleaved layout the TRMM streams:
 //   Kt2[((k >> 1) * mc + c) * 2 + (k & 1)] = s * exp(-sum beta (X[k] - Xs[c])^2)
@@ -102,12 +104,20 @@ GP_DEV void glds16(const double* g, double* l) {
 __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
     const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt2,
     int mc, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
-    int NI, int NC) {
+    int NI, int NC, int order) {
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const int b = blockIdx.y;
-  const int t = blockIdx.x;
-  const int I = NI - 1 - t / NC;     // heaviest row tiles dispatch first
-  const int C = t % NC;
+  int t = blockIdx.x;
+  int I, C;
+  if (order == 0 || order == 3) {    // row-major: heaviest row tiles of every panel first
+    if (order == 3) t = xcd_remap(t, NI * NC);   // ... consecutive panels of a row on one XCD
+    I = NI - 1 - t / NC;
+    C = t % NC;
+  } else {                           // panel-major: all row tiles of a test-point panel
+    if (order == 2) t = xcd_remap(t, NI * NC);   // ... on one XCD (shares the B panel in L2)
+    C = t / NI;
+    I = NI - 1 - t % NI;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
@@ -244,6 +254,18 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
                                batch, st);
 }
 
+// Tile order of trmm_reduce: 0 row-major (tiles sharing an L^-1 row panel run together),
+// 1 panel-major, 2 panel-major + XCD remap, 3 row-major + XCD remap.  Measured on MI355X
+// (tools/sweep_trmm.sh, profiles/r01): row-major wins (66 TF/s at C3 vs 36-58 for the
+// panel-major orders).  GPFIT_TRMM_ORDER overrides the default for experiments.
+int trmm_order() {
+  static int v = [] {
+    const char* e = getenv("GPFIT_TRMM_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 struct Plan {
   int npad, NI, mc, NC, nchunks;
   long long off_z, off_kt, off_part, bytes;
@@ -258,8 +280,11 @@ Plan make_plan(int n, int m, int batch, int m_chunk) {
   if (m_chunk > 0) {
     mc = gp_ceil_div(m_chunk, BC) * BC;
   } else {
+    // 4096 test points per chunk measured best at C3 and C4 (tools/sweep_trmm.sh); shrink
+    // only when the batch's cross-covariance slab would exceed kDefaultChunkElems doubles
     long long cap = kDefaultChunkElems / ((long long)p.npad * (batch > 0 ? batch : 1));
     mc = (int)((cap / BC) * BC);
+    if (mc > kDefaultChunk) mc = kDefaultChunk;
     if (mc < BC) mc = BC;
   }
   if (mc > mpad) mc = mpad;
@@ -336,7 +361,7 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
     gpfit_prof_begin(GP_PROF_TRMM, stream);
     hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0,
                        stream, Linv, ldinv, strideInv, kt, p.mc, sK, z, p.npad, part, p.NI,
-                       ncol_tiles);
+                       ncol_tiles, trmm_order());
     gpfit_prof_end(GP_PROF_TRMM, stream);
     GP_CK(hipGetLastError());
     hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0,

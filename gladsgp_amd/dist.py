@@ -93,16 +93,18 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
 def gather_rows(ctx: Context, local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:
     """Gather variable-length row blocks (dim 0) to rank 0; returns the concatenation there.
 
-    Blocks are padded to the largest count so one collective (all_gather of equal shapes)
-    serves RCCL and gloo alike; rank 0 trims and concatenates.
+    Blocks are padded to the largest count so a single equal-shape ``gather`` serves RCCL and
+    gloo alike (only rank 0 receives: one message per rank over xGMI, no all-to-all);
+    rank 0 trims and concatenates, the other ranks get None.
     """
     if not ctx.distributed:
         return local
     mx = max(counts)
     pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
-    bufs = [torch.empty_like(pad) for _ in range(ctx.world)]
-    dist.all_gather(bufs, pad)
+    if local.shape[0]:
+        pad[: local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in range(ctx.world)] if ctx.rank == 0 else None
+    dist.gather(pad, gather_list=bufs, dst=0)
     if ctx.rank != 0:
         return None
     return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)

@@ -275,22 +275,11 @@ class EmulatorPrediction:
         else:
             mean_l = torch.empty((0, self.m), dtype=F64, device=dev)
             var_l = torch.empty((0, self.m), dtype=F64, device=dev)
-        if ctx is not None and ctx.distributed:
-            counts = [len(gdist.shard_units(len(units), r, world)) for r in range(world)]
-            both = torch.stack([mean_l, var_l], dim=1) if mean_l.shape[0] else \
-                torch.empty((0, 2, self.m), dtype=F64, device=dev)
-            allb = gdist.gather_rows(ctx, both, counts)
-            if allb is None:
-                self.w_dev = self.var_dev = None
-                return
-            order = np.concatenate([gdist.shard_units(len(units), r, world)
-                                    for r in range(world)])
-            inv = np.empty_like(order)
-            inv[order] = np.arange(len(order))
-            allb = allb[torch.as_tensor(inv, device=allb.device)]
-            mean_u, var_u = allb[:, 0], allb[:, 1]
-        else:
-            mean_u, var_u = mean_l, var_l
+        both = assemble_units(ctx, mean_l, var_l, len(units))
+        if both is None:
+            self.w_dev = self.var_dev = None
+            return
+        mean_u, var_u = both
         # units are (s, j) in s-major order -> (S, P, m) -> (S, m, P)
         self.w_dev = mean_u.reshape(S, P, self.m).permute(0, 2, 1).contiguous()
         self.var_dev = var_u.reshape(S, P, self.m).permute(0, 2, 1).contiguous()
@@ -326,6 +315,29 @@ class EmulatorPrediction:
         if not std:
             y = blas.standardize(y.contiguous(), sd_.y_mean, sd_.y_sd, inverse=True)
         return y.reshape(S, m, -1).cpu().numpy()
+
+
+def assemble_units(ctx, mean_l: torch.Tensor, var_l: torch.Tensor, n_units: int):
+    """Gather per-rank (mean, var) rows of round-robin-dealt units back into unit order.
+
+    Single process: identity.  Distributed: one gather to rank 0 (RCCL on GPUs, gloo on CPU);
+    returns None on the other ranks.
+    """
+    if ctx is None or not ctx.distributed:
+        return mean_l, var_l
+    world = ctx.world
+    m = mean_l.shape[1]
+    counts = [len(gdist.shard_units(n_units, r, world)) for r in range(world)]
+    both = torch.stack([mean_l, var_l], dim=1) if mean_l.shape[0] else \
+        torch.empty((0, 2, m), dtype=mean_l.dtype, device=mean_l.device)
+    allb = gdist.gather_rows(ctx, both, counts)
+    if allb is None:
+        return None
+    order = np.concatenate([gdist.shard_units(n_units, r, world) for r in range(world)])
+    inv = np.empty_like(order)
+    inv[order] = np.arange(len(order))
+    allb = allb[torch.as_tensor(inv, device=allb.device)]
+    return allb[:, 0], allb[:, 1]
 
 
 # SEPIA-compatible alias for drop-in call sites
