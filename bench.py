@@ -186,10 +186,16 @@ def main():
     tr_cnt, tr_ms = prof["trmm"]
     tr_flops = float(m) * K * (n * n + 4 * n)
     tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12
+    traffic, traffic_src = None, None
+    tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    if os.path.exists(tf) and n == 4096 and args.m_chunk in (0, 4096):
+        tj = json.load(open(tf))
+        traffic = tj["kernels"]["trmm_reduce_kernel"]["bytes_per_launch"]
+        traffic_src = "profiles/r01/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
     roof = {"kernel": "trmm_reduce_kernel", "bound": "mfma", "achieved": round(tr_tfs, 3),
             "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
-            "traffic": None, "launches": tr_cnt,
+            "traffic": traffic, "traffic_source": traffic_src, "launches": tr_cnt,
             "avg_launch_ms": round(tr_ms / max(tr_cnt, 1), 4),
             "flop_per_launch": tr_flops / max(tr_cnt, 1),
             "work_note": "n^2 + 4n flop per prediction (lower-triangular L^-1 K*^T + mean/var)"}
