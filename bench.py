@@ -7,7 +7,9 @@
 
 A step is one full pass of the hot path for one GP on one GPU, from hyperparameters to
 answers: ARD-SE Gram (n x n) -> blocked MFMA Cholesky + L^-1 -> fused cross-covariance /
-TRMM / mean+variance over that rank's m = 100k test points.  Inputs are HBM-resident before
+TRMM / mean+variance over that rank's m = 100k test points.  Within a step the
+cross-covariance (independent of the factorisation) is built on a second HIP stream while
+the latency-bound Cholesky runs (``--serial`` disables that); steps never overlap.  Inputs are HBM-resident before
 the timed region.  Ranks are independent test-point shards of one trained GP (weak scaling:
 every rank predicts its own 100k points; no collective inside a step), so
 value = N * 100k * K / max-over-ranks(time).
@@ -130,6 +132,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds for the CPU leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workload", choices=("c3", "c4"), default="c3")
+    ap.add_argument("--serial", action="store_true",
+                    help="c3: no side-stream overlap of cross-covariance and factorisation")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
     args = ap.parse_args()
     if args.workload == "c4":
@@ -150,10 +154,15 @@ def main():
     var = torch.empty((1, m), dtype=torch.float64, device=dev)
 
     def step():
-        G = kernels.gram(Xd, bd, sd, dd)
-        ch = kernels.cholesky_inverse(G)
-        kernels.predict(ch, Xd, Xsd, bd, sd, sd, yd, m_chunk=args.m_chunk, workspace=ws,
-                        out=(mean, var))
+        if args.serial:
+            G = kernels.gram(Xd, bd, sd, dd)
+            ch = kernels.cholesky_inverse(G)
+            kernels.predict(ch, Xd, Xsd, bd, sd, sd, yd, m_chunk=args.m_chunk, workspace=ws,
+                            out=(mean, var))
+            return ch
+        # cross-covariance on a side stream while the factorisation runs (within one step)
+        _, _, ch = kernels.fit_predict(Xd, Xsd, bd, sd, dd, sd, yd, m_chunk=args.m_chunk,
+                                       workspace=ws, out=(mean, var))
         return ch
 
     for _ in range(args.warmup):

@@ -36,6 +36,12 @@ SIGNATURES = {
     "gp_predict": (c_int, [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_int, c_int,
                            c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int, c_void_p]),
+    "gp_predict_prepared_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
+    "gp_predict_cross": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                 c_int, c_void_p, c_int, c_void_p, c_ll, c_int, c_void_p]),
+    "gp_predict_solve": (c_int, [c_void_p, c_int, c_ll, c_int, c_int, c_void_p, c_void_p, c_int,
+                                 c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int,
+                                 c_void_p]),
     "gp_trmv": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
                         c_void_p]),
     "gp_nll": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p,

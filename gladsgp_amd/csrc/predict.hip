@@ -267,11 +267,13 @@ int trmm_order() {
 }
 
 struct Plan {
-  int npad, NI, mc, NC, nchunks;
-  long long off_z, off_kt, off_part, bytes;
+  int npad, NI, mc, NC, nchunks, slabs;
+  long long off_z, off_kt, off_part, bytes, slab_elems;
 };
 
-Plan make_plan(int n, int m, int batch, int m_chunk) {
+// slabs = 1: one cross-covariance chunk at a time (gp_predict); slabs = nchunks: every chunk
+// materialised up front (gp_predict_cross + gp_predict_solve).
+Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
   Plan p;
   p.npad = gp_padded_n(n);
   p.NI = p.npad / BI;
@@ -292,8 +294,10 @@ Plan make_plan(int n, int m, int batch, int m_chunk) {
   p.mc = mc;
   p.NC = mc / BC;
   p.nchunks = gp_ceil_div(m, mc);
+  p.slabs = all_slabs ? p.nchunks : 1;
+  p.slab_elems = (long long)batch * mc * p.npad;
   long long z = (long long)batch * p.npad;
-  long long kt = (long long)batch * mc * p.npad;
+  long long kt = p.slab_elems * p.slabs;
   long long part = (long long)batch * 2 * p.NI * mc;
   p.off_z = 0;
   p.off_kt = ((z * 8 + 255) / 256) * 256;
@@ -309,16 +313,15 @@ extern "C" long long gp_predict_ws_bytes(int n, int m, int batch, int m_chunk) {
   return make_plan(n, m, batch, m_chunk).bytes;
 }
 
-extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, const double* X,
-                          int ldx, const double* Xs, int ldxs, int n, int m, int d,
-                          const double* beta, int ldbeta, const double* s,
-                          const double* s_pred, const double* w_hat, int ldw, double* mean,
-                          double* var, int ldo, int batch, void* ws, long long ws_bytes,
-                          int m_chunk, hipStream_t stream) {
-  if (!Linv || (reinterpret_cast<uintptr_t>(Linv) & 15)) return -1;
-  const int npad = gp_padded_n(n);
-  if (ldinv < npad || ldinv < 1 || (ldinv & 1)) return -2;   // 16-B aligned double2 loads
-  if ((batch > 1 && strideInv < (long long)ldinv * npad) || (strideInv & 1)) return -3;
+extern "C" long long gp_predict_prepared_ws_bytes(int n, int m, int batch, int m_chunk) {
+  if (n <= 0 || m <= 0 || batch <= 0) return 0;
+  return make_plan(n, m, batch, m_chunk, true).bytes;
+}
+
+namespace {
+
+int check_common(const double* X, int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                 const double* beta, int ldbeta, const double* s, int batch) {
   if (!X) return -4;
   if (ldx < d) return -5;
   if (!Xs) return -6;
@@ -329,45 +332,140 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
   if (!beta) return -11;
   if (ldbeta < d && batch > 1) return -12;
   if (!s) return -13;
+  if (batch < 0) return -20;
+  return 0;
+}
+
+int check_solve(const double* Linv, int ldinv, long long strideInv, int n, const double* s_pred,
+                const double* w_hat, int ldw, int m, double* mean, double* var, int ldo,
+                int batch) {
+  if (!Linv || (reinterpret_cast<uintptr_t>(Linv) & 15)) return -1;
+  const int npad = gp_padded_n(n);
+  if (ldinv < npad || ldinv < 1 || (ldinv & 1)) return -2;   // 16-B aligned double2 loads
+  if ((batch > 1 && strideInv < (long long)ldinv * npad) || (strideInv & 1)) return -3;
   if (!s_pred) return -14;
   if (!w_hat) return -15;
   if (ldw < n && batch > 1) return -16;
   if (!mean) return -17;
   if (!var) return -18;
   if (ldo < m && batch > 1) return -19;
-  if (batch < 0) return -20;
+  return 0;
+}
+
+struct WS {
+  double *z, *kt, *part;
+};
+
+WS carve(const Plan& p, void* ws) {
+  char* base = static_cast<char*>(ws);
+  return {reinterpret_cast<double*>(base + p.off_z), reinterpret_cast<double*>(base + p.off_kt),
+          reinterpret_cast<double*>(base + p.off_part)};
+}
+
+hipError_t cross_chunk(const Plan& p, int ch, double* kt, const double* X, int ldx,
+                       const double* Xs, int ldxs, int n, int m, int d, const double* beta,
+                       int ldbeta, const double* s, int batch, hipStream_t stream) {
+  const int c0 = ch * p.mc;
+  const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
+  gpfit_prof_begin(GP_PROF_CROSS, stream);
+  hipError_t e = cross_kp_launch(X, n, ldx, Xs + (long long)c0 * ldxs, mv, ldxs, d, beta,
+                                 ldbeta, s, kt, p.mc, p.npad, (long long)p.mc * p.npad, batch,
+                                 stream);
+  gpfit_prof_end(GP_PROF_CROSS, stream);
+  return e;
+}
+
+hipError_t solve_chunk(const Plan& p, int ch, const WS& w, const double* kt, const double* Linv,
+                       int ldinv, long long strideInv, int m, const double* s_pred,
+                       double* mean, double* var, int ldo, int batch, hipStream_t stream) {
+  const int c0 = ch * p.mc;
+  const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
+  const int ncol_tiles = gp_ceil_div(mv, BC);
+  gpfit_prof_begin(GP_PROF_TRMM, stream);
+  hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0, stream,
+                     Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, w.z, p.npad,
+                     w.part, p.NI, ncol_tiles, trmm_order());
+  gpfit_prof_end(GP_PROF_TRMM, stream);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0, stream,
+                     w.part, p.NI, p.mc, mv, s_pred, mean, var, ldo, c0);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, const double* X,
+                          int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                          const double* beta, int ldbeta, const double* s,
+                          const double* s_pred, const double* w_hat, int ldw, double* mean,
+                          double* var, int ldo, int batch, void* ws, long long ws_bytes,
+                          int m_chunk, hipStream_t stream) {
+  int rc = check_common(X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch);
+  if (rc) return rc;
+  rc = check_solve(Linv, ldinv, strideInv, n, s_pred, w_hat, ldw, m, mean, var, ldo, batch);
+  if (rc) return rc;
   if (n == 0 || m == 0 || batch == 0) return 0;
+  if (m_chunk < 0) return -23;
   const Plan p = make_plan(n, m, batch, m_chunk);
   if (!ws) return -21;
   if (ws_bytes < p.bytes) return -22;
-  if (m_chunk < 0) return -23;
-  char* base = static_cast<char*>(ws);
-  double* z = reinterpret_cast<double*>(base + p.off_z);
-  double* kt = reinterpret_cast<double*>(base + p.off_kt);
-  double* part = reinterpret_cast<double*>(base + p.off_part);
+  const WS w = carve(p, ws);
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
-  GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, z, p.npad, p.npad, n, batch,
+  GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
                           stream));
-  const long long sK = (long long)p.mc * p.npad;
   for (int ch = 0; ch < p.nchunks; ++ch) {
-    const int c0 = ch * p.mc;
-    const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
-    gpfit_prof_begin(GP_PROF_CROSS, stream);
-    GP_CK(cross_kp_launch(X, n, ldx, Xs + (long long)c0 * ldxs, mv, ldxs, d, beta, ldbeta, s,
-                          kt, p.mc, p.npad, sK, batch, stream));
-    gpfit_prof_end(GP_PROF_CROSS, stream);
-    const int ncol_tiles = gp_ceil_div(mv, BC);
-    gpfit_prof_begin(GP_PROF_TRMM, stream);
-    hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0,
-                       stream, Linv, ldinv, strideInv, kt, p.mc, sK, z, p.npad, part, p.NI,
-                       ncol_tiles, trmm_order());
-    gpfit_prof_end(GP_PROF_TRMM, stream);
-    GP_CK(hipGetLastError());
-    hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0,
-                       stream, part, p.NI, p.mc, mv, s_pred, mean, var, ldo, c0);
-    GP_CK(hipGetLastError());
+    GP_CK(cross_chunk(p, ch, w.kt, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch, stream));
+    GP_CK(solve_chunk(p, ch, w, w.kt, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch,
+                      stream));
   }
+#undef GP_CK
+  return 0;
+}
+
+extern "C" int gp_predict_cross(const double* X, int ldx, const double* Xs, int ldxs, int n,
+                                int m, int d, const double* beta, int ldbeta, const double* s,
+                                int batch, void* ws, long long ws_bytes, int m_chunk,
+                                hipStream_t stream) {
+  int rc = check_common(X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch);
+  if (rc) return rc;
+  if (n == 0 || m == 0 || batch == 0) return 0;
+  if (m_chunk < 0) return -23;
+  const Plan p = make_plan(n, m, batch, m_chunk, true);
+  if (!ws) return -21;
+  if (ws_bytes < p.bytes) return -22;
+  const WS w = carve(p, ws);
+  for (int ch = 0; ch < p.nchunks; ++ch) {
+    hipError_t e = cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n,
+                               m, d, beta, ldbeta, s, batch, stream);
+    if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  }
+  return 0;
+}
+
+extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideInv, int n,
+                                int m, const double* s_pred, const double* w_hat, int ldw,
+                                double* mean, double* var, int ldo, int batch, void* ws,
+                                long long ws_bytes, int m_chunk, hipStream_t stream) {
+  if (n < 0) return -4;
+  if (m < 0) return -5;
+  if (batch < 0) return -12;
+  int rc = check_solve(Linv, ldinv, strideInv, n, s_pred, w_hat, ldw, m, mean, var, ldo, batch);
+  if (rc) return rc;
+  if (n == 0 || m == 0 || batch == 0) return 0;
+  if (m_chunk < 0) return -23;
+  const Plan p = make_plan(n, m, batch, m_chunk, true);
+  if (!ws) return -21;
+  if (ws_bytes < p.bytes) return -22;
+  const WS w = carve(p, ws);
+  hipError_t e;
+#define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
+  GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
+                          stream));
+  for (int ch = 0; ch < p.nchunks; ++ch)
+    GP_CK(solve_chunk(p, ch, w, w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
+                      s_pred, mean, var, ldo, batch, stream));
 #undef GP_CK
   return 0;
 }

@@ -212,3 +212,87 @@ def trmv(chol: Cholesky, w) -> torch.Tensor:
     _capi.call("gp_trmv", chol.linv_buf.data_ptr(), npad, npad * npad, n, w_t.data_ptr(), n,
                z.data_ptr(), n, batch, _stream(dev))
     return z
+
+
+@dataclass
+class Prepared:
+    """Cross-covariance of every test-point chunk, built by :func:`predict_prepare`."""
+
+    n: int
+    m: int
+    batch: int
+    m_chunk: int
+    ws: torch.Tensor
+
+
+def predict_prepare(X: torch.Tensor, Xs: torch.Tensor, beta, s, batch: int = 1,
+                    m_chunk: int = 0, workspace: PredictWorkspace | None = None) -> Prepared:
+    """Phase 1 of predict (gp_predict_cross): independent of the factorisation, so it can run
+    on a side stream while :func:`cholesky_inverse` runs."""
+    dev = X.device
+    X = _as_f64(X, dev, "X")
+    Xs = _as_f64(Xs, dev, "Xs")
+    n, d = X.shape
+    m = Xs.shape[0]
+    beta_t = _beta(beta, batch, d, dev)
+    s_t = _per_batch(s, batch, dev, "s")
+    nbytes = _capi.lib().gp_predict_prepared_ws_bytes(n, m, batch, int(m_chunk))
+    ws = (workspace or PredictWorkspace()).get(nbytes, dev)
+    _capi.call("gp_predict_cross", X.data_ptr(), d, Xs.data_ptr(), d, n, m, d, beta_t.data_ptr(),
+               d, s_t.data_ptr(), batch, ws.data_ptr(), ws.numel(), int(m_chunk), _stream(dev))
+    return Prepared(n, m, batch, int(m_chunk), ws)
+
+
+def predict_solve(chol: Cholesky, prep: Prepared, s_pred, w,
+                  out: tuple[torch.Tensor, torch.Tensor] | None = None):
+    """Phase 2 of predict (gp_predict_solve): mean / variance from a prepared cross-cov."""
+    dev = chol.linv_buf.device
+    batch, npad = chol.linv_buf.shape[0], chol.linv_buf.shape[1]
+    n, m = chol.n, prep.m
+    if prep.n != n or prep.batch != batch:
+        raise ValueError("prepared cross-covariance does not match the factorisation")
+    sp_t = _per_batch(s_pred, batch, dev, "s_pred")
+    w_t = _as_f64(w, dev, "w").reshape(batch, n)
+    if out is None:
+        mean = torch.empty((batch, m), dtype=F64, device=dev)
+        var = torch.empty((batch, m), dtype=F64, device=dev)
+    else:
+        mean, var = out
+    _capi.call("gp_predict_solve", chol.linv_buf.data_ptr(), npad, npad * npad, n, m,
+               sp_t.data_ptr(), w_t.data_ptr(), n, mean.data_ptr(), var.data_ptr(),
+               mean.stride(0) if batch > 1 else m, batch, prep.ws.data_ptr(), prep.ws.numel(),
+               prep.m_chunk, _stream(dev))
+    return mean, var
+
+
+_SIDE: dict = {}
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    key = str(device)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
+def fit_predict(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
+                workspace: PredictWorkspace | None = None, out=None):
+    """Gram -> Cholesky/L^-1 -> predict for ``batch`` GPs with the cross-covariance built on a
+    side stream concurrently with the (latency-bound) factorisation.  Returns (mean, var, chol).
+    """
+    dev = X.device
+    bt = torch.as_tensor(beta)
+    batch = bt.shape[0] if bt.dim() == 2 else 1
+    main = torch.cuda.current_stream(dev)
+    side = side_stream(dev)
+    ws = workspace or PredictWorkspace()
+    n, m = X.shape[0], Xs.shape[0]
+    ws.get(_capi.lib().gp_predict_prepared_ws_bytes(n, m, batch, int(m_chunk)), dev)
+    side.wait_stream(main)                       # inputs and workspace are ready
+    with torch.cuda.stream(side):
+        prep = predict_prepare(X, Xs, beta, s, batch, m_chunk, ws)
+    G = gram(X, beta, s, delta, batch=batch)
+    ch = cholesky_inverse(G)
+    main.wait_stream(side)
+    mean, var = predict_solve(ch, prep, s_pred, w, out=out)
+    return mean, var, ch

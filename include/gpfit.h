@@ -100,6 +100,23 @@ int gp_predict(const double* Linv, int ldinv, long long strideInv,
                int batch, void* ws, long long ws_bytes, int m_chunk, hipStream_t stream);
 
 /*
+ * Two-phase form of gp_predict.  The cross-covariance of every test-point chunk does not depend
+ * on the factorisation, so it can be built on a second stream while gp_potrf_inv runs:
+ *   gp_predict_cross : Kt chunks for all m points into ws (X, Xs, beta, s only)
+ *   gp_predict_solve : z = Linv w, TRMM + mean/var per chunk from the prepared ws
+ * Both take the same (n, m, batch, m_chunk) and a workspace of
+ * gp_predict_prepared_ws_bytes(n, m, batch, m_chunk) bytes; results equal gp_predict's.
+ */
+long long gp_predict_prepared_ws_bytes(int n, int m, int batch, int m_chunk);
+int gp_predict_cross(const double* X, int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                     const double* beta, int ldbeta, const double* s, int batch,
+                     void* ws, long long ws_bytes, int m_chunk, hipStream_t stream);
+int gp_predict_solve(const double* Linv, int ldinv, long long strideInv, int n, int m,
+                     const double* s_pred, const double* w_hat, int ldw, double* mean,
+                     double* var, int ldo, int batch, void* ws, long long ws_bytes,
+                     int m_chunk, hipStream_t stream);
+
+/*
  * z_b = Linv_b w_b (lower-triangular gemv, n rows), z_b = z + b*ldz.
  * Building block of the likelihood (quadratic form w^T A^-1 w = ||z||^2).
  */

@@ -241,3 +241,26 @@ def test_cpu_tensor_rejected(dev):
     from gladsgp_amd import kernels
     with pytest.raises(ValueError):
         kernels.gram(torch.zeros(4, 2, dtype=torch.float64), [1.0, 1.0], 1.0, 0.0)
+
+
+def test_two_phase_predict_and_overlap_match_single(dev):
+    """gp_predict_cross + gp_predict_solve (and the side-stream fit_predict) == gp_predict."""
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(21)
+    n, m, d, B = 333, 5000, 8, 3
+    X, Xs = rng.random((n, d)), rng.random((m, d))
+    betas = rng.uniform(0.5, 4, (B, d))
+    s = rng.uniform(0.5, 2, B)
+    delta = rng.uniform(1e-5, 1e-3, B)
+    W = rng.standard_normal((B, n))
+    Xd, Xsd = _t(X, dev), _t(Xs, dev)
+    ch = kernels.cholesky_inverse(kernels.gram(Xd, _t(betas, dev), _t(s, dev), _t(delta, dev)))
+    m1, v1 = kernels.predict(ch, Xd, Xsd, _t(betas, dev), _t(s, dev), _t(s, dev), _t(W, dev),
+                             m_chunk=1024)
+    prep = kernels.predict_prepare(Xd, Xsd, _t(betas, dev), _t(s, dev), batch=B, m_chunk=1024)
+    m2, v2 = kernels.predict_solve(ch, prep, _t(s, dev), _t(W, dev))
+    assert torch.equal(m1, m2) and torch.equal(v1, v2)
+    m3, v3, _ = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                    _t(s, dev), _t(W, dev), m_chunk=1024)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m3) and torch.equal(v1, v3)
