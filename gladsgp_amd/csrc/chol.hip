@@ -37,10 +37,15 @@ constexpr int LP = NB + 1;  // LDS pitch (doubles)
 struct __align__(16) Smem {
   double As[NB * LP];
   double Bs[NB * LP];
-  double VA[2][NB];    // step vector V (L column below the pivot, R row at and left of it)
+  double VA[2][NB];    // L[.][j]   of the current pair (rows below the pivot)
+  double VB[2][NB];    // L[.][j+1]
+  double RR[2][NB];    // R[j][.]   (unscaled, c <= j)
+  double RB[2][NB];    // R[j+1][.] (unscaled, c <= j+1)
   double sps[NB];      // L_jj
   double invs[NB];     // 1 / L_jj
   double inv[2];
+  double inv1[2];
+  double l10[2];
   double red[4];
   int bad[NB];         // per-column non-PD pivot flags (written once, scanned at the end)
   int fail;
@@ -126,14 +131,17 @@ GP_DEV void store_tile(double* Cs, const f64x4 (&acc)[2][2], double* __restrict_
 //
 // Thread (row i = t & 63, wave cq = t >> 6) owns the 16 register slots w[u] of columns
 // c = 16 cq + u.  Slot c holds A[i][c] until column c is factored and R[i][c] afterwards
-// (R starts as I; X = L^-1 has rows R_i. / L_ii), so step j is one update per slot:
-//   w[c] -= L[i][j] * V[c]              for c > j,  V[c] = L[c][j]
-//   w[c] -= (L[i][j] / L_jj) * V[c]     for c <= j, V[c] = R[j][c] (unscaled, V[j] = 1)
-// The two halves of V come from disjoint writers (the wave owning column j: lanes c > j;
-// lane j of every wave: its slots c <= j), so V is one LDS vector, ping-ponged, and a step is
-// one barrier + 16 FMAs per thread.  The j loop is unrolled by 16 so the owner wave and slot
-// of column j are compile-time; there is no early exit (a failure is flagged, the sweep
-// finishes on garbage that is discarded) so the unroll always happens.
+// (R starts as I; X = L^-1 has rows R_i. / L_ii).  Columns are taken TWO at a time (a rank-2
+// right-looking step): the wave owning columns (j, j+1) factors its 2x2 pivot block in
+// registers (readlane pivots, rsqrt, the local column-j update of column j+1) and publishes
+//   VA0 = L[.][j], VA1 = L[.][j+1]   (lanes below the pivots)     and    inv0, inv1, L[j+1][j]
+// while lanes j and j+1 of every wave publish their R rows (unscaled).  After one barrier each
+// thread applies, per slot c (the c-vs-j tests are wave-uniform),
+//   c > j+1 :  A[i][c] -= L[i][j] L[c][j] + L[i][j+1] L[c][j+1]
+//   c <= j+1:  R[i][c] -= L[i][j] X[j][c] + L[i][j+1] X[j+1][c]
+// with X[j][c] = R[j][c]/L_jj and X[j+1][c] = (R[j+1][c] - L[j+1][j] X[j][c]) / L_j+1,j+1.
+// 32 barriers per block instead of 64; the owner's two pivot chains per step are the critical
+// path.  The pair loop is unrolled by 8 so owner wave and slots are compile-time.
 GP_DEV int diag_factor_inv(Smem& sm, double* T, double* U, int nb, double* ld_out) {
   const int tid = threadIdx.x;
   const int i = tid & (NB - 1);
@@ -143,80 +151,94 @@ GP_DEV int diag_factor_inv(Smem& sm, double* T, double* U, int nb, double* ld_ou
 #pragma unroll
   for (int u = 0; u < 16; ++u) w[u] = T[i * LP + cb + u];
 
-  // publish step j's V / pivot (owner wave of column j, slot uj, pivot already computed by
-  // every wave from its own slot uj: only the owner's copy is the real one) and the R row
-  auto publish = [&](int j, int own, int uj, int q, double piv, double inv) {
+  // publish pair (j, j+1): owner wave `own`, slots uj, uj+1 (compile-time), buffer q
+  auto publish = [&](int j, int own, int uj, int q) {
     if (cq == own) {
-      if (i > j) {
-        const double l = w[uj] * inv;                // L[i][j]
-        sm.VA[q][i] = l;
-        T[i * LP + j] = l;                           // T's column j was read only by this wave
-      }
-      w[uj] = (i == j) ? 1.0 : 0.0;                  // slot j now holds R[i][j] (= delta_ij)
+      const double a0 = w[uj];
+      const double piv0 = readlane_f64(a0, j);
+      const double inv0 = rsqrt_nr(piv0);
+      const double l0 = (i > j) ? a0 * inv0 : 0.0;               // L[i][j]
+      const double L10 = readlane_f64(l0, j + 1);                 // L[j+1][j]
+      const double a1 = fma(-l0, L10, w[uj + 1]);                 // A[i][j+1] after column j
+      const double piv1 = readlane_f64(a1, j + 1);
+      const double inv1 = rsqrt_nr(piv1);
+      const double l1 = (i > j + 1) ? a1 * inv1 : 0.0;           // L[i][j+1]
+      sm.VA[q][i] = l0;
+      sm.VB[q][i] = l1;
+      if (i > j) T[i * LP + j] = l0;                             // T's columns j, j+1 were read
+      if (i > j + 1) T[i * LP + j + 1] = l1;                     // only by this wave
+      w[uj] = (i == j) ? 1.0 : 0.0;                              // slots now hold R (= delta)
+      w[uj + 1] = (i == j + 1) ? 1.0 : 0.0;
       if (i == 0) {
-        sm.inv[q] = inv;
-        sm.invs[j] = inv;
-        sm.sps[j] = piv * inv;
-        sm.bad[j] = (!(piv > 0.0) || !isfinite(piv)) ? 1 : 0;
+        sm.inv[q] = inv0;
+        sm.inv1[q] = inv1;
+        sm.l10[q] = L10;
+        sm.invs[j] = inv0;
+        sm.invs[j + 1] = inv1;
+        sm.sps[j] = piv0 * inv0;
+        sm.sps[j + 1] = piv1 * inv1;
+        sm.bad[j] = (!(piv0 > 0.0) || !isfinite(piv0)) ? 1 : 0;
+        sm.bad[j + 1] = (!(piv1 > 0.0) || !isfinite(piv1)) ? 1 : 0;
       }
     }
-    // R[j][c] for c <= j (V[j] = 1): all 16 slots of waves left of the owner, slots u <= uj
-    // of the owner (uj is compile-time) — two uniform cases, no per-slot branches
-    if (i == j) {
+    // R rows j (c <= j) and j+1 (c <= j+1), unscaled; two uniform cases per wave
+    if (i == j || i == j + 1) {
+      double* dst = (i == j) ? sm.RR[q] : sm.RB[q];
       if (cq < own) {
 #pragma unroll
         for (int u = 0; u < 16; u += 2) {
           double2 y;
           y.x = w[u];
           y.y = w[u + 1];
-          *reinterpret_cast<double2*>(&sm.VA[q][cb + u]) = y;
+          *reinterpret_cast<double2*>(&dst[cb + u]) = y;
         }
       } else if (cq == own) {
 #pragma unroll
         for (int u = 0; u < 16; ++u)
-          if (u <= uj) sm.VA[q][cb + u] = w[u];
+          if (u <= uj + 1) dst[cb + u] = w[u];
       }
     }
   };
 
-  {
-    const double piv = readlane_f64(w[0], 0);
-    publish(0, 0, 0, 0, piv, rsqrt_nr(piv));
-  }
+  publish(0, 0, 0, 0);
 #pragma unroll 1
   for (int jb = 0; jb < NB / 16; ++jb) {
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
+    for (int jj = 0; jj < 16; jj += 2) {
       const int j = jb * 16 + jj;
-      const int p = jj & 1;
+      const int p = (jj >> 1) & 1;
       __syncthreads();
-      const double inv = sm.inv[p];
-      const double vi = sm.VA[p][i];
-      const double m1 = (i > j) ? vi : 0.0;          // L[i][j]
-      const double m2 = m1 * inv;                    // L[i][j] / L_jj
-      double v[16];
+      const double inv0 = sm.inv[p], inv1 = sm.inv1[p], L10 = sm.l10[p];
+      const double m0 = (i > j) ? sm.VA[p][i] : 0.0;             // L[i][j]
+      const double m1 = (i > j + 1) ? sm.VB[p][i] : 0.0;         // L[i][j+1]
+      // next pair's owner / slots (compile-time per jj); its two slots are updated first
+      const int own1 = (jj < 14) ? jb : jb + 1, u1 = (jj + 2) & 15;
 #pragma unroll
-      for (int u = 0; u < 16; u += 2) {
-        const double2 x = *reinterpret_cast<const double2*>(&sm.VA[p][cb + u]);
-        v[u] = x.x;
-        v[u + 1] = x.y;
-      }
-      // slot u1 first in every wave: in the owner of column j+1 it carries the next pivot, whose
-      // readlane -> rsqrt chain then overlaps the other 15 FMAs (straight-line code)
-      const int own1 = (jj < 15) ? jb : jb + 1, u1 = (jj + 1) & 15;
-      w[u1] = fma(-((cb + u1 > j) ? m1 : m2), v[u1], w[u1]);
-      double piv1 = 0.0, inv1 = 0.0;
-      if (j + 1 < NB) {
-        piv1 = readlane_f64(w[u1], j + 1);
-        inv1 = rsqrt_nr(piv1);
-      }
+      for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        if (u == u1) continue;
-        const int c = cb + u;
-        w[u] = fma(-((c > j) ? m1 : m2), v[u], w[u]);
+        for (int u = 0; u < 16; u += 2) {
+          const bool first = (cq == own1) && (u == u1);
+          if ((pass == 0) != first) continue;
+          const int c = cb + u;                                    // c, c+1 same side of j+1
+          if (c > j + 1) {
+            const double2 a = *reinterpret_cast<const double2*>(&sm.VA[p][c]);
+            const double2 b = *reinterpret_cast<const double2*>(&sm.VB[p][c]);
+            w[u] = fma(-m1, b.x, fma(-m0, a.x, w[u]));
+            w[u + 1] = fma(-m1, b.y, fma(-m0, a.y, w[u + 1]));
+          } else {
+            const double2 r0 = *reinterpret_cast<const double2*>(&sm.RR[p][c]);
+            const double2 r1 = *reinterpret_cast<const double2*>(&sm.RB[p][c]);
+            // X[j][c] (zero for c = j+1), X[j+1][c]
+            const double x0a = r0.x * inv0;
+            const double x0b = (c + 1 <= j) ? r0.y * inv0 : 0.0;
+            const double x1a = (r1.x - L10 * x0a) * inv1;
+            const double x1b = (r1.y - L10 * x0b) * inv1;
+            w[u] = fma(-m1, x1a, fma(-m0, x0a, w[u]));
+            w[u + 1] = fma(-m1, x1b, fma(-m0, x0b, w[u + 1]));
+          }
+        }
       }
-      if (j + 1 < NB) publish(j + 1, own1, u1, p ^ 1, piv1, inv1);
+      if (j + 2 < NB) publish(j + 2, own1, u1, p ^ 1);
     }
   }
   __syncthreads();
