@@ -8,14 +8,23 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libgpfit.so")
 SOURCES = ["gram.hip", "chol.hip", "predict.hip", "linalg.hip", "profile.hip", "blas.hip",
            "eig.hip"]
+# Per-file extra flags.  chol.hip: MFMA accumulators in VGPRs (not AGPRs) so the update
+# kernel, whose lookahead block calls the ~250-VGPR diagonal factor, keeps 2 waves/SIMD; and
+# 16-byte LDS reads (ds_read_b128) for the factor's broadcast rows.
+EXTRA = {"chol.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form",
+                      "-Xclang", "-target-feature", "-Xclang", "+enable-ds128"]}
+OBJ_DIR = os.path.join(PKG_DIR, "_obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+         "-Wno-unused-function"]
 
 
 def _stale() -> bool:
@@ -31,10 +40,21 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     """Compile every HIP source for gfx950 into one shared library; return its path."""
     if not force and not _stale():
         return LIB_PATH
-    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(OBJ_DIR, src.replace(".hip", ".o"))
+        cmd = [HIPCC] + FLAGS + EXTRA.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB_PATH + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", "-Wno-unused-function", "-o", tmp] + srcs
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -15,18 +15,18 @@
 // own update (diag_factor_inv below), so each step is two launches (panel, update+diag) and the
 // serial diagonal work overlaps the rest of the trailing update.
 //
-// diag_factor_inv: 4 waves, register resident (see the function for the scheme): X = L^-1
-// comes out of the same right-looking sweep as L (X_j. = R_j. / L_jj, R_i. -= L_ij X_j.),
-// one barrier and 16 FMAs per thread per column step.
+// diag_factor_inv: barrier-free symmetric elimination in one wave's registers (L), with a
+// second wave applying the same row operations to I (L^-1); see the function.
 #include "gpfit_common.h"
 #include "gpfit_profile.h"
 #include "../../include/gpfit.h"
 
-#ifdef GPFIT_DIAG_STAMPS
-__device__ unsigned long long gpfit_diag_stamps[16];
-extern "C" int gp_diag_stamps(unsigned long long* host16) {
-  return (int)hipMemcpyFromSymbol(host16, HIP_SYMBOL(gpfit_diag_stamps), 16 * 8);
-}
+#ifdef GPFIT_DIAG_PROBE
+__device__ unsigned long long gpfit_diag_probe[8];
+#define DIAG_STAMP(w, k) \
+  do { if ((threadIdx.x & 63) == 0 && wv == (w)) gpfit_diag_probe[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define DIAG_STAMP(w, k) do { } while (0)
 #endif
 
 namespace {
@@ -37,35 +37,71 @@ constexpr int LP = NB + 1;  // LDS pitch (doubles)
 struct __align__(16) Smem {
   double As[NB * LP];
   double Bs[NB * LP];
-  double VA[2][NB];    // L[.][j]   of the current pair (rows below the pivot)
-  double VB[2][NB];    // L[.][j+1]
-  double RR[2][NB];    // R[j][.]   (unscaled, c <= j)
-  double RB[2][NB];    // R[j+1][.] (unscaled, c <= j+1)
-  double sps[NB];      // L_jj
   double invs[NB];     // 1 / L_jj
-  double inv[2];
-  double inv1[2];
-  double l10[2];
   double red[4];
-  int bad[NB];         // per-column non-PD pivot flags (written once, scanned at the end)
+  int step;            // diag sweep: elimination steps published by wave 0
   int fail;
 };
 
-// S[k][x]: NAT → src[x + k*ld] (x contiguous), TRN → src[k + x*ld] (k contiguous).
-template <bool TRN>
-GP_DEV void stage(double* S, const double* __restrict__ src, int ld, int xv, int kv) {
-#pragma unroll 4
-  for (int q = 0; q < (NB * NB) / 256; ++q) {
-    const int g = threadIdx.x + 256 * q;
-    const int fast = g & (NB - 1), slow = g >> 6;
-    if (!TRN) {
-      const int x = fast, k = slow;
-      S[k * LP + x] = (x < xv && k < kv) ? src[x + (long long)k * ld] : 0.0;
-    } else {
-      const int k = fast, x = slow;
-      S[k * LP + x] = (x < xv && k < kv) ? src[k + (long long)x * ld] : 0.0;
+// Operand tiles go global -> registers -> LDS in two phases so every load of a tile (and of
+// the other operand) is in flight at once; the tile is walked as (fast, slow) index pairs with
+// fast contiguous in memory, as 16-byte loads when the tile is full and aligned.
+//   NAT: S[k][x] = src[x + k*ld] (fast = x),   TRN: S[k][x] = src[k + x*ld] (fast = k).
+struct OpTile {
+  double v[16];
+};
+
+GP_DEV void load_op(OpTile& t, const double* __restrict__ src, int ld, int fv, int sv) {
+  const int tid = threadIdx.x;
+  const bool full = fv == NB && sv == NB && (ld & 1) == 0 && (((size_t)src & 15) == 0);
+  if (full) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int g = tid + 256 * q;
+      const int f = (g & 31) * 2, sl = g >> 5;
+      const double2 x = *reinterpret_cast<const double2*>(src + f + (long long)sl * ld);
+      t.v[2 * q] = x.x;
+      t.v[2 * q + 1] = x.y;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int g = tid + 256 * q;
+      const int f = (g & 31) * 2, sl = g >> 5;
+      const bool ok = sl < sv;
+      t.v[2 * q] = (ok && f < fv) ? src[f + (long long)sl * ld] : 0.0;
+      t.v[2 * q + 1] = (ok && f + 1 < fv) ? src[f + 1 + (long long)sl * ld] : 0.0;
     }
   }
+}
+
+template <bool TRN>
+GP_DEV void store_op(double* S, const OpTile& t) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int g = tid + 256 * q;
+    const int f = (g & 31) * 2, sl = g >> 5;
+    if (!TRN) {
+      S[sl * LP + f] = t.v[2 * q];
+      S[sl * LP + f + 1] = t.v[2 * q + 1];
+    } else {
+      S[f * LP + sl] = t.v[2 * q];
+      S[(f + 1) * LP + sl] = t.v[2 * q + 1];
+    }
+  }
+}
+
+// As <- op A (NAT, x < av, k < kv), Bs <- op B (NAT or TRN, x < bv, k < kv)
+template <bool TRNB>
+GP_DEV void stage2(double* As, const double* __restrict__ A, int lda, int av, double* Bs,
+                   const double* __restrict__ B, int ldb, int bv, int kv) {
+  OpTile ta, tb;
+  load_op(ta, A, lda, av, kv);
+  if (!TRNB) load_op(tb, B, ldb, bv, kv);
+  else load_op(tb, B, ldb, kv, bv);
+  store_op<false>(As, ta);
+  store_op<TRNB>(Bs, tb);
 }
 
 // acc (this wave's 32x32) = sum_k As[k][rows] * Bs[k][cols]
@@ -124,145 +160,135 @@ GP_DEV void store_tile(double* Cs, const f64x4 (&acc)[2][2], double* __restrict_
   }
 }
 
-// Factor + invert the 64x64 tile held (full, symmetric) in T[row * LP + col]; all 256 threads
-// call it.  nb valid rows (rows/cols >= nb are identity padding).  On return T holds L (lower,
-// zero upper), U holds L^-1 (lower, zero upper); returns 0 or the 1-based local index of the
-// first non-PD pivot.
+using LdsSmem = __attribute__((address_space(3))) Smem;
+
+// The one LDS block of every kernel in this file, at namespace scope so that it has the same
+// fixed address in all of them and diag_factor_inv (a separate function) addresses it with
+// immediate offsets instead of a runtime base register.
+__shared__ Smem g_sm;
+using lds_double = __attribute__((address_space(3))) double;
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+using lds_dvec2 = __attribute__((address_space(3))) const dvec2;
+
+// y[r] -= v[r] * x for r in [R0, NB), v[r] read as 16-byte LDS broadcasts from V (v[r] at
+// V[r]), 8 reads per batch with the next batch in flight while the current one is consumed.
+// Rows below R0 are untouched (R0 may be odd: the pair holding R0 - 1 is read, half used).
+template <int R0>
+GP_DEV void bcast_axpy(double (&y)[NB], const lds_double* V, double x) {
+  constexpr int P0 = R0 & ~1;              // first pair
+  constexpr int NP = (NB - P0) / 2;        // pairs
+  constexpr int BATCH = 8;
+  static_for<0, NP, BATCH>([&](auto Bt) {
+    constexpr int b0 = decltype(Bt)::value;
+    constexpr int nb = (NP - b0 < BATCH) ? NP - b0 : BATCH;
+    dvec2 v[BATCH];
+    static_for<0, nb, 1>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      v[q] = *reinterpret_cast<lds_dvec2*>(&V[P0 + 2 * (b0 + q)]);
+    });
+    static_for<0, nb, 1>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      constexpr int r = P0 + 2 * (b0 + q);
+      if constexpr (r >= R0) y[r] = fma(-v[q].x, x, y[r]);
+      y[r + 1] = fma(-v[q].y, x, y[r + 1]);
+    });
+  });
+}
+
+// Factor + invert the 64x64 tile held (full, symmetric) in T = sm.As[row * LP + col]; all 256
+// threads call it.  nb valid rows (rows/cols >= nb are identity padding).  On return T holds L
+// (lower, zero upper), U = sm.Bs holds L^-1 (lower, zero upper); returns 0 or the 1-based local
+// index of the first non-PD pivot.
 //
-// Thread (row i = t & 63, wave cq = t >> 6) owns the 16 register slots w[u] of columns
-// c = 16 cq + u.  Slot c holds A[i][c] until column c is factored and R[i][c] afterwards
-// (R starts as I; X = L^-1 has rows R_i. / L_ii).  Columns are taken TWO at a time (a rank-2
-// right-looking step): the wave owning columns (j, j+1) factors its 2x2 pivot block in
-// registers (readlane pivots, rsqrt, the local column-j update of column j+1) and publishes
-//   VA0 = L[.][j], VA1 = L[.][j+1]   (lanes below the pivots)     and    inv0, inv1, L[j+1][j]
-// while lanes j and j+1 of every wave publish their R rows (unscaled).  After one barrier each
-// thread applies, per slot c (the c-vs-j tests are wave-uniform),
-//   c > j+1 :  A[i][c] -= L[i][j] L[c][j] + L[i][j+1] L[c][j+1]
-//   c <= j+1:  R[i][c] -= L[i][j] X[j][c] + L[i][j+1] X[j+1][c]
-// with X[j][c] = R[j][c]/L_jj and X[j+1][c] = (R[j+1][c] - L[j+1][j] X[j][c]) / L_j+1,j+1.
-// 32 barriers per block instead of 64; the owner's two pivot chains per step are the critical
-// path.  The pair loop is unrolled by 8 so owner wave and slots are compile-time.
-GP_DEV int diag_factor_inv(Smem& sm, double* T, double* U, int nb, double* ld_out) {
+// Symmetric Gaussian elimination A = Lt D Lt^T (Lt unit lower), no barriers inside the sweep:
+//  * wave 0 holds the whole tile, lane c = column c (w[r] = A[r][c], 64 registers), and runs the
+//    64 elimination steps.  Step j: pivot p = A[j][j], t_c = A[j][c] / p (lanes c > j, else 0),
+//    A[r][c] -= A[r][j] t_c for r > j.  The trailing block stays symmetric, so A[r][j] is lane
+//    r's own row-j value: every lane writes w[j] to LDS row S[j] and the column comes back as
+//    16-byte broadcast reads (A[j+1][j], which the next pivot needs, goes by readlane).
+//    Critical path per column: readlane -> rcp + 2 Newton -> t -> one FMA; the broadcast reads
+//    are issued before the chain.  Lane c's column freezes after step c and then holds
+//    Lt[.][c] p_c, so L[r][c] = w[r] / sqrt(p_c).  t goes to LDS as the multiplier row M[j]
+//    with a step counter after it.
+//  * wave 1 applies the same row operations to I, lane c = column c of B:
+//    B[r][c] -= M[j][r] B[j][c] (r > j), M[j] read as broadcasts, following the counter.
+//    B = Lt^-1 and L^-1 = D^-1/2 B.
+// Waves 2-3 only take part in the barriers.  S lives in T's storage (T is in registers during
+// the sweep), M in U's (U is written after the barrier that ends both sweeps).
+// noinline: inlined into a kernel that also has rolled loops, the 64-step straight-line sweep
+// sends LLVM's CodeGenPrepare quadratic (minutes of compile time); as a callee it compiles alone.
+__device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out) {
+  LdsSmem& sm = *(LdsSmem*)&g_sm;
   const int tid = threadIdx.x;
-  const int i = tid & (NB - 1);
-  const int cq = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cb = cq * 16;
-  double w[16];
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  lds_double* T = sm.As;
+  lds_double* S = sm.As;
+  lds_double* M = sm.Bs;
+  if (tid == 0) sm.step = 0;
+  __syncthreads();
+  DIAG_STAMP(0, 0);
+  if (wv == 0) {
+    double w[NB];
 #pragma unroll
-  for (int u = 0; u < 16; ++u) w[u] = T[i * LP + cb + u];
-
-  // publish pair (j, j+1): owner wave `own`, slots uj, uj+1 (compile-time), buffer q
-  auto publish = [&](int j, int own, int uj, int q) {
-    if (cq == own) {
-      const double a0 = w[uj];
-      const double piv0 = readlane_f64(a0, j);
-      const double inv0 = rsqrt_nr(piv0);
-      const double l0 = (i > j) ? a0 * inv0 : 0.0;               // L[i][j]
-      const double L10 = readlane_f64(l0, j + 1);                 // L[j+1][j]
-      const double a1 = fma(-l0, L10, w[uj + 1]);                 // A[i][j+1] after column j
-      const double piv1 = readlane_f64(a1, j + 1);
-      const double inv1 = rsqrt_nr(piv1);
-      const double l1 = (i > j + 1) ? a1 * inv1 : 0.0;           // L[i][j+1]
-      sm.VA[q][i] = l0;
-      sm.VB[q][i] = l1;
-      if (i > j) T[i * LP + j] = l0;                             // T's columns j, j+1 were read
-      if (i > j + 1) T[i * LP + j + 1] = l1;                     // only by this wave
-      w[uj] = (i == j) ? 1.0 : 0.0;                              // slots now hold R (= delta)
-      w[uj + 1] = (i == j + 1) ? 1.0 : 0.0;
-      if (i == 0) {
-        sm.inv[q] = inv0;
-        sm.inv1[q] = inv1;
-        sm.l10[q] = L10;
-        sm.invs[j] = inv0;
-        sm.invs[j + 1] = inv1;
-        sm.sps[j] = piv0 * inv0;
-        sm.sps[j + 1] = piv1 * inv1;
-        sm.bad[j] = (!(piv0 > 0.0) || !isfinite(piv0)) ? 1 : 0;
-        sm.bad[j + 1] = (!(piv1 > 0.0) || !isfinite(piv1)) ? 1 : 0;
+    for (int r = 0; r < NB; ++r) w[r] = T[r * LP + lane];
+    __syncthreads();   // every wave has read T before S overwrites it
+    double piv = 1.0;
+    static_for<0, NB, 1>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      const double wj = w[j];
+      const double p = readlane_f64(wj, j);
+      piv = (lane == j) ? p : piv;
+      if constexpr (j + 1 < NB) {
+        S[j * NB + lane] = wj;
+        const double t = (lane > j) ? wj * rcp_nr(p) : 0.0;
+        w[j + 1] = fma(-readlane_f64(w[j + 1], j), t, w[j + 1]);
+        M[j * NB + lane] = t;
+        if constexpr (j + 2 < NB) bcast_axpy<j + 2>(w, &S[j * NB], t);
+        __hip_atomic_store((int*)&sm.step, j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+    });
+    DIAG_STAMP(0, 1);
+    const double rs = rsqrt_nr(piv);
+    sm.invs[lane] = rs;
+    const bool badc = lane < nb && (!(piv > 0.0) || !isfinite(piv));
+    const unsigned long long badm = __ballot(badc);
+    double lg = (lane < nb) ? log(piv) : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
+    if (lane == 0) {
+      sm.fail = badm ? __ffsll((long long)badm) : 0;
+      sm.red[0] = lg;
     }
-    // R rows j (c <= j) and j+1 (c <= j+1), unscaled; two uniform cases per wave
-    if (i == j || i == j + 1) {
-      double* dst = (i == j) ? sm.RR[q] : sm.RB[q];
-      if (cq < own) {
 #pragma unroll
-        for (int u = 0; u < 16; u += 2) {
-          double2 y;
-          y.x = w[u];
-          y.y = w[u + 1];
-          *reinterpret_cast<double2*>(&dst[cb + u]) = y;
-        }
-      } else if (cq == own) {
+    for (int r = 0; r < NB; ++r)
+      T[r * LP + lane] = (r > lane) ? w[r] * rs : ((r == lane) ? piv * rs : 0.0);
+    __syncthreads();
+  } else if (wv == 1) {
+    __syncthreads();
+    double bq[NB];
 #pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (u <= uj + 1) dst[cb + u] = w[u];
-      }
-    }
-  };
-
-  publish(0, 0, 0, 0);
-#pragma unroll 1
-  for (int jb = 0; jb < NB / 16; ++jb) {
+    for (int r = 0; r < NB; ++r) bq[r] = (r == lane) ? 1.0 : 0.0;
+    static_for<0, NB - 1, 1>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      constexpr int PE = 4;   // poll wave 0's step counter every PE steps
+      if constexpr (j % PE == 0)
+        lds_wait_ge((int*)&sm.step, (j + PE < NB - 1) ? j + PE : NB - 1);
+      bcast_axpy<j + 1>(bq, &M[j * NB], bq[j]);
+    });
+    DIAG_STAMP(1, 2);
+    __syncthreads();   // invs from wave 0; every M read done
 #pragma unroll
-    for (int jj = 0; jj < 16; jj += 2) {
-      const int j = jb * 16 + jj;
-      const int p = (jj >> 1) & 1;
-      __syncthreads();
-      const double inv0 = sm.inv[p], inv1 = sm.inv1[p], L10 = sm.l10[p];
-      const double m0 = (i > j) ? sm.VA[p][i] : 0.0;             // L[i][j]
-      const double m1 = (i > j + 1) ? sm.VB[p][i] : 0.0;         // L[i][j+1]
-      // next pair's owner / slots (compile-time per jj); its two slots are updated first
-      const int own1 = (jj < 14) ? jb : jb + 1, u1 = (jj + 2) & 15;
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-        for (int u = 0; u < 16; u += 2) {
-          const bool first = (cq == own1) && (u == u1);
-          if ((pass == 0) != first) continue;
-          const int c = cb + u;                                    // c, c+1 same side of j+1
-          if (c > j + 1) {
-            const double2 a = *reinterpret_cast<const double2*>(&sm.VA[p][c]);
-            const double2 b = *reinterpret_cast<const double2*>(&sm.VB[p][c]);
-            w[u] = fma(-m1, b.x, fma(-m0, a.x, w[u]));
-            w[u + 1] = fma(-m1, b.y, fma(-m0, a.y, w[u + 1]));
-          } else {
-            const double2 r0 = *reinterpret_cast<const double2*>(&sm.RR[p][c]);
-            const double2 r1 = *reinterpret_cast<const double2*>(&sm.RB[p][c]);
-            // X[j][c] (zero for c = j+1), X[j+1][c]
-            const double x0a = r0.x * inv0;
-            const double x0b = (c + 1 <= j) ? r0.y * inv0 : 0.0;
-            const double x1a = (r1.x - L10 * x0a) * inv1;
-            const double x1b = (r1.y - L10 * x0b) * inv1;
-            w[u] = fma(-m1, x1a, fma(-m0, x0a, w[u]));
-            w[u + 1] = fma(-m1, x1b, fma(-m0, x0b, w[u + 1]));
-          }
-        }
-      }
-      if (j + 2 < NB) publish(j + 2, own1, u1, p ^ 1);
-    }
+    for (int r = 0; r < NB; ++r) sm.Bs[r * LP + lane] = bq[r] * sm.invs[r];
+  } else {
+    __syncthreads();
+    __syncthreads();
   }
   __syncthreads();
-  if (tid < 64) {
-    const unsigned long long badm = __ballot(sm.bad[tid] != 0 && tid < nb);
-    if (tid == 0) sm.fail = badm ? (__ffsll((long long)badm)) : 0;
-  }
-  __syncthreads();
-  const int f = sm.fail;              // first bad pivot among the nb valid columns
-  if (f) return f;
-  const double inv_i = sm.invs[i];
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int c = cb + u;
-    U[i * LP + c] = (c <= i) ? w[u] * inv_i : 0.0;
-    if (c >= i) T[i * LP + c] = (c == i) ? sm.sps[i] : 0.0;   // c < i: written by publish
-  }
-  double lg = (cq == 0 && i < nb) ? 2.0 * log(sm.sps[i]) : 0.0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
-  if ((tid & 63) == 0) sm.red[tid >> 6] = lg;
-  __syncthreads();
-  if (ld_out) *ld_out = (sm.red[0] + sm.red[1]) + (sm.red[2] + sm.red[3]);
-  return 0;
+  DIAG_STAMP(0, 3);
+  const int f = sm.fail;
+  if (ld_out) *ld_out = sm.red[0];
+  return f;
 }
 
 // Factor diagonal block k whose (updated, symmetric) tile is in sm.As as [row][col]; write
@@ -271,7 +297,7 @@ GP_DEV void diag_block(Smem& sm, double* __restrict__ Ab, int lda, double* __res
                        int ldx, int n, int k, int* info, double* logdet, int b) {
   const int k0 = k * NB, nb = min(NB, n - k0);
   double lg = 0.0;
-  const int f = diag_factor_inv(sm, sm.As, sm.Bs, nb, &lg);
+  const int f = diag_factor_inv(nb, &lg);
   if (f) {
     if (threadIdx.x == 0 && info) info[b] = k0 + f;
     return;
@@ -290,12 +316,12 @@ GP_DEV void diag_block(Smem& sm, double* __restrict__ Ab, int lda, double* __res
   }
 }
 
-__global__ __launch_bounds__(256) void chol_diag_kernel(
+__global__ __launch_bounds__(256, 2) void chol_diag_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
     long long sX, int n, int k, int* __restrict__ info, double* __restrict__ logdet) {
   const int b = blockIdx.x;
   if (info && info[b] != 0) return;
-  __shared__ Smem sm;
+  Smem& sm = g_sm;
   const int k0 = k * NB, nb = min(NB, n - k0);
   double* Ab = A + b * sA;
   const double* Akk = Ab + k0 + (long long)k0 * lda;
@@ -319,7 +345,7 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
     long long sX, int n, int k, int nbelow, const int* __restrict__ info) {
   const int b = blockIdx.y;
   if (info && info[b] != 0) return;
-  __shared__ Smem sm;
+  Smem& sm = g_sm;
   const int k0 = k * NB, kv = min(NB, n - k0);
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
@@ -329,8 +355,7 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
     // L_ik = A_ik D_k^T :  opA[r][p] = A_ik(r,p) (NAT), opB[p][c] = D_k(c,p) (NAT)
     const int i0 = (k + 1 + blockIdx.x) * NB, rv = min(NB, n - i0);
     double* Aik = Ab + i0 + (long long)k0 * lda;
-    stage<false>(sm.As, Aik, lda, rv, kv);
-    stage<false>(sm.Bs, Dk, ldx, kv, kv);
+    stage2<false>(sm.As, Aik, lda, rv, sm.Bs, Dk, ldx, kv, kv);
     __syncthreads();
     mma64(sm.As, sm.Bs, acc);
     store_tile(sm.As, acc, Aik, lda, rv, kv);
@@ -338,8 +363,7 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
     // X_kc = D_k R_kc :  opA[r][p] = D_k(r,p) (NAT), opB[p][c] = R_kc(p,c) (TRN)
     const int c0 = (blockIdx.x - nbelow) * NB;
     double* Rkc = Xb + k0 + (long long)c0 * ldx;
-    stage<false>(sm.As, Dk, ldx, kv, kv);
-    stage<true>(sm.Bs, Rkc, ldx, NB, kv);
+    stage2<true>(sm.As, Dk, ldx, kv, sm.Bs, Rkc, ldx, NB, kv);
     __syncthreads();
     mma64(sm.As, sm.Bs, acc);
     store_tile(sm.As, acc, Rkc, ldx, kv, NB);
@@ -347,12 +371,12 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
 }
 
 // Trailing update of step k.  Block 0 owns tile (k+1, k+1) and then factors it (lookahead).
-__global__ __launch_bounds__(256) void chol_update_kernel(
+__global__ __launch_bounds__(256, 2) void chol_update_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
     long long sX, int n, int k, int T, int* __restrict__ info, double* __restrict__ logdet) {
   const int b = blockIdx.y;
   if (info && info[b] != 0) return;
-  __shared__ Smem sm;
+  Smem& sm = g_sm;
   const int k0 = k * NB, kv = min(NB, n - k0);
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
@@ -399,9 +423,8 @@ __global__ __launch_bounds__(256) void chol_update_kernel(
     const bool ok = row < rv && col < cv && (!diag || row >= col);
     cpre[q] = ok ? Cp[row + (long long)col * ldc] : 0.0;
   }
-  stage<false>(sm.As, Ap, lda, rv, kv);
-  if (trn) stage<true>(sm.Bs, Bp, ldb, NB, kv);
-  else stage<false>(sm.Bs, Bp, ldb, cv, kv);
+  if (trn) stage2<true>(sm.As, Ap, lda, rv, sm.Bs, Bp, ldb, NB, kv);
+  else stage2<false>(sm.As, Ap, lda, rv, sm.Bs, Bp, ldb, cv, kv);
   __syncthreads();
   f64x4 acc[2][2];
   mma64(sm.As, sm.Bs, acc);

@@ -8,6 +8,7 @@
 //   C/D(16x16): lane l, reg r holds C[(l >> 4) + 4 r][l & 15]
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -42,6 +43,48 @@ GP_DEV double rsqrt_nr(double x) {
   y = y * fma(-hx * y, y, 1.5);
   y = y * fma(-hx * y, y, 1.5);
   return y;
+}
+
+// 1/x: hardware v_rcp_f64 estimate + two Newton steps (<= 1 ulp typical).
+GP_DEV double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = fma(y, fma(-x, y, 1.0), y);
+  y = fma(y, fma(-x, y, 1.0), y);
+  return y;
+}
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i = B, B+S, ... < E (register
+// arrays indexed by i stay in registers whatever the unroller decides).
+template <int B, int E, int S, class F>
+GP_DEV void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + S, E, S>(f);
+  }
+}
+
+// Spin (s_sleep between polls) until the LDS int *flag >= target.  Written as one asm block so
+// it is opaque to the compiler: a visible loop splits the caller's straight-line, register-
+// array code into basic blocks and the allocator then spills.  The memory clobber keeps the
+// caller's later LDS reads below the wait.  The low 32 bits of a flat LDS address are its
+// LDS offset (the shared aperture is 4 GiB aligned).
+GP_DEV void lds_wait_ge(int* flag, int target) {
+  const unsigned addr = (unsigned)(size_t)flag;
+  int v;
+  unsigned s;
+  asm volatile(
+      "1:\n"
+      "  ds_read_b32 %0, %2\n"
+      "  s_waitcnt lgkmcnt(0)\n"
+      "  v_readfirstlane_b32 %1, %0\n"
+      "  s_cmp_ge_i32 %1, %3\n"
+      "  s_cbranch_scc1 2f\n"
+      "  s_sleep 1\n"
+      "  s_branch 1b\n"
+      "2:\n"
+      : "=&v"(v), "=&s"(s)
+      : "v"(addr), "s"(target)
+      : "memory", "scc");
 }
 
 GP_DEV f64x4 zero4() { f64x4 z = {0.0, 0.0, 0.0, 0.0}; return z; }
