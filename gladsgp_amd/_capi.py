@@ -46,6 +46,10 @@ SIGNATURES = {
                         c_void_p]),
     "gp_nll": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p,
                        c_void_p, c_int, c_void_p]),
+    "gp_loglik_ws_bytes": (c_ll, [c_int, c_int]),
+    "gp_loglik": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                          c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,
+                          c_void_p]),
     "gp_dgemm_ws_bytes": (c_ll, [c_int, c_int, c_int]),
     "gp_dgemm": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.c_double, c_void_p, c_int,
                          c_void_p, c_int, ctypes.c_double, c_void_p, c_int, c_void_p, c_ll,

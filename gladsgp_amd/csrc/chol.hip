@@ -171,26 +171,35 @@ typedef double dvec2 __attribute__((ext_vector_type(2)));
 using lds_dvec2 = __attribute__((address_space(3))) const dvec2;
 
 // y[r] -= v[r] * x for r in [R0, NB), v[r] read as 16-byte LDS broadcasts from V (v[r] at
-// V[r]), 8 reads per batch with the next batch in flight while the current one is consumed.
+// V[r]) in batches of 8, software-pipelined: batch b+1 is issued before batch b is consumed.
 // Rows below R0 are untouched (R0 may be odd: the pair holding R0 - 1 is read, half used).
 template <int R0>
 GP_DEV void bcast_axpy(double (&y)[NB], const lds_double* V, double x) {
   constexpr int P0 = R0 & ~1;              // first pair
   constexpr int NP = (NB - P0) / 2;        // pairs
   constexpr int BATCH = 8;
-  static_for<0, NP, BATCH>([&](auto Bt) {
-    constexpr int b0 = decltype(Bt)::value;
+  constexpr int NBT = (NP + BATCH - 1) / BATCH;
+  dvec2 buf[2][BATCH];
+  auto load = [&](auto Bt) {
+    constexpr int bt = decltype(Bt)::value;
+    constexpr int b0 = bt * BATCH;
     constexpr int nb = (NP - b0 < BATCH) ? NP - b0 : BATCH;
-    dvec2 v[BATCH];
     static_for<0, nb, 1>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
-      v[q] = *reinterpret_cast<lds_dvec2*>(&V[P0 + 2 * (b0 + q)]);
+      buf[bt & 1][q] = *reinterpret_cast<lds_dvec2*>(&V[P0 + 2 * (b0 + q)]);
     });
+  };
+  load(std::integral_constant<int, 0>{});
+  static_for<0, NBT, 1>([&](auto Bt) {
+    constexpr int bt = decltype(Bt)::value;
+    if constexpr (bt + 1 < NBT) load(std::integral_constant<int, bt + 1>{});
+    constexpr int b0 = bt * BATCH;
+    constexpr int nb = (NP - b0 < BATCH) ? NP - b0 : BATCH;
     static_for<0, nb, 1>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       constexpr int r = P0 + 2 * (b0 + q);
-      if constexpr (r >= R0) y[r] = fma(-v[q].x, x, y[r]);
-      y[r + 1] = fma(-v[q].y, x, y[r + 1]);
+      if constexpr (r >= R0) y[r] = fma(-buf[bt & 1][q].x, x, y[r]);
+      y[r + 1] = fma(-buf[bt & 1][q].y, x, y[r + 1]);
     });
   });
 }
@@ -228,6 +237,11 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
   if (tid == 0) sm.step = 0;
   __syncthreads();
   DIAG_STAMP(0, 0);
+#if defined(GPFIT_DIAG_VARIANT) && GPFIT_DIAG_VARIANT == 3
+  if (tid == 0) sm.fail = 0;
+  __syncthreads();
+  return 0;
+#endif
   if (wv == 0) {
     double w[NB];
 #pragma unroll
@@ -266,6 +280,11 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
     __syncthreads();
   } else if (wv == 1) {
     __syncthreads();
+#if defined(GPFIT_DIAG_VARIANT) && GPFIT_DIAG_VARIANT == 1
+    __syncthreads();
+    __syncthreads();
+    return 0;
+#endif
     double bq[NB];
 #pragma unroll
     for (int r = 0; r < NB; ++r) bq[r] = (r == lane) ? 1.0 : 0.0;
@@ -485,10 +504,16 @@ extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
   if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
-  // zero L^-1 (upper triangle + padding), one 2-D memset per problem
-  for (int b = 0; b < batch; ++b)
-    GP_CK(hipMemset2DAsync(Linv + b * strideInv, sizeof(double) * ldinv, 0,
-                           sizeof(double) * npad, npad, stream));
+  // zero L^-1 (upper triangle + padding): one memset for a packed batch, else one 2-D memset
+  // per problem
+  if (ldinv == npad && (batch == 1 || strideInv == (long long)npad * npad)) {
+    GP_CK(hipMemsetAsync(Linv, 0, sizeof(double) * ((long long)(batch - 1) * strideInv +
+                                                    (long long)ldinv * npad), stream));
+  } else {
+    for (int b = 0; b < batch; ++b)
+      GP_CK(hipMemset2DAsync(Linv + b * strideInv, sizeof(double) * ldinv, 0,
+                             sizeof(double) * npad, npad, stream));
+  }
   const int N = gp_ceil_div(n, NB);
   gpfit_prof_begin(GP_PROF_POTRF, stream);
   hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, stream, A, lda, strideA,

@@ -43,9 +43,13 @@ __global__ __launch_bounds__(1024) void trmv_kernel(const double* __restrict__ L
   }
 }
 
+// out[b] = sign * (1/2 ||z_b||^2 + 1/2 logdet[b]); a problem whose factorisation failed
+// (info[b] != 0, when info is given) gets sign * +inf.
 __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restrict__ z, int ldz,
                                                          int n,
                                                          const double* __restrict__ logdet,
+                                                         const int* __restrict__ info,
+                                                         double sign,
                                                          double* __restrict__ nll) {
   const int b = blockIdx.x;
   const double* zb = z + (long long)b * ldz;
@@ -56,7 +60,10 @@ __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restric
   __shared__ double red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) nll[b] = 0.5 * ((red[0] + red[1]) + (red[2] + red[3])) + 0.5 * logdet[b];
+  if (threadIdx.x == 0) {
+    const double v = 0.5 * ((red[0] + red[1]) + (red[2] + red[3])) + 0.5 * logdet[b];
+    nll[b] = sign * ((info && info[b] != 0) ? __builtin_huge_val() : v);
+  }
 }
 
 }  // namespace
@@ -103,7 +110,84 @@ extern "C" int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
   hipError_t e = gpfit_trmv_launch(Linv, ldinv, strideInv, w, ldw, work, n, n, n, batch, stream);
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   hipLaunchKernelGGL(nll_reduce_kernel, dim3(batch), dim3(256), 0, stream, work, n, n, logdet,
-                     nll);
+                     (const int*)nullptr, 1.0, nll);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+namespace {
+struct LoglikWs {
+  double* G;
+  double* Linv;
+  double* z;
+  double* logdet;
+  int* info;
+  long long bytes;
+};
+
+LoglikWs loglik_carve(void* ws, int n, int batch) {
+  const long long npad = gp_padded_n(n);
+  auto up = [](long long b) { return (b + 255) & ~255LL; };
+  LoglikWs w;
+  char* p = static_cast<char*>(ws);
+  long long off = 0;
+  w.G = reinterpret_cast<double*>(p + off);
+  off += up(8LL * batch * n * n);
+  w.Linv = reinterpret_cast<double*>(p + off);
+  off += up(8LL * batch * npad * npad);
+  w.z = reinterpret_cast<double*>(p + off);
+  off += up(8LL * batch * n);
+  w.logdet = reinterpret_cast<double*>(p + off);
+  off += up(8LL * batch);
+  w.info = reinterpret_cast<int*>(p + off);
+  off += up(4LL * batch);
+  w.bytes = off;
+  return w;
+}
+}  // namespace
+
+extern "C" long long gp_loglik_ws_bytes(int n, int batch) {
+  if (n < 0 || batch < 0) return -1;
+  return loglik_carve(nullptr, n, batch).bytes;
+}
+
+extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* beta,
+                         int ldbeta, const double* s, const double* delta, const double* w,
+                         int ldw, int batch, void* ws, long long ws_bytes, double* ll,
+                         int* info, hipStream_t stream) {
+  if (!X) return -1;
+  if (n < 0) return -2;
+  if (d < 1) return -3;
+  if (ldx < d) return -4;
+  if (!beta) return -5;
+  if (ldbeta < d) return -6;
+  if (!s) return -7;
+  if (!delta) return -8;
+  if (!w) return -9;
+  if (ldw < n && batch > 1) return -10;
+  if (batch < 0) return -11;
+  if (n == 0 || batch == 0) return 0;
+  if (!ws) return -12;
+  const LoglikWs c = loglik_carve(ws, n, batch);
+  if (ws_bytes < c.bytes) return -13;
+  if (!ll) return -14;
+  const int npad = gp_padded_n(n);
+  int rc = gp_gram_ardse(X, n, d, ldx, beta, ldbeta, s, delta, c.G, n, (long long)n * n, batch,
+                         stream);
+  if (rc) return rc;
+  rc = gp_potrf_inv(c.G, n, n, (long long)n * n, c.Linv, npad, (long long)npad * npad, batch,
+                    c.info, c.logdet, stream);
+  if (rc) return rc;
+  hipError_t e = gpfit_trmv_launch(c.Linv, npad, (long long)npad * npad, w, ldw, c.z, n, n, n,
+                                   batch, stream);
+  if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  hipLaunchKernelGGL(nll_reduce_kernel, dim3(batch), dim3(256), 0, stream, c.z, n, n, c.logdet,
+                     (const int*)c.info, -1.0, ll);
+  e = hipGetLastError();
+  if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  if (info) {
+    e = hipMemcpyAsync(info, c.info, sizeof(int) * batch, hipMemcpyDeviceToDevice, stream);
+    if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  }
+  return 0;
 }

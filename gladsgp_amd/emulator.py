@@ -34,7 +34,9 @@ import torch
 
 from . import blas, kernels
 from . import dist as gdist
+from . import mcmc
 from .blas import CM, gemm
+from .mcmc import ModelParams, SepiaParam  # noqa: F401  (re-exported for drop-in imports)
 
 F64 = torch.float64
 
@@ -130,14 +132,38 @@ class EmulatorModel:
         self.LamSim = lam
         self.n, self.d = sd_.t.shape
         self.P = sd_.K.shape[0]
-        # GPMSA default starting values (SEPIA's defaults; step sizes 03...ipynb:192-208)
-        self.params = {
-            "betaU": np.full((self.d + 1, self.P), 0.1),
-            "lamUz": np.ones((1, self.P)),
-            "lamWs": np.full((1, self.P), 1000.0),
-            "lamWOs": np.full((1, 1), 1000.0),
-        }
+        # GPMSA default starting values, priors and steps (see gladsgp_amd.mcmc)
+        self.params = ModelParams(self.d, self.P)
         self.samples = None
+        self.rng = np.random.default_rng()
+        self._chain = None            # device chain state carried from tuning into sampling
+
+    # ---------------------------------------------------------------------------- sampling
+    def _sampler(self) -> mcmc.GPUSampler:
+        return mcmc.GPUSampler(self.data.sim_data.t, self.w_hat.transpose(0, 1).contiguous(),
+                               self.LamSim, self.params)
+
+    def tune_step_sizes(self, n_burn, n_levels, prog=False, diagnostics=False,
+                        update_vals=True):
+        """SEPIA tune_step_sizes (src/model.py:234): per-element Metropolis step sizes from
+        n_levels x n_burn sweeps on the GPU (algorithm: gladsgp_amd.mcmc module doc)."""
+        sm = self._sampler()
+        st = mcmc.tune_step_sizes(sm, int(n_burn), int(n_levels), self.rng)
+        if update_vals:
+            sm.write_back(st)
+        self._chain = None
+
+    def do_mcmc(self, nsamp, prog=False, do_propMH=True, no_init=False):
+        """SEPIA do_mcmc (src/model.py:235): ``nsamp`` component-wise Metropolis sweeps on the
+        GPU, appended to ``samples`` (betaU (N, (d+1) P), lamUz/lamWs (N, P), lamWOs (N, 1),
+        logPost (N, 1)); the last state becomes the current parameter values."""
+        sm = self._sampler()
+        st, new = sm.run(int(nsamp), self.rng)
+        sm.write_back(st)
+        if self.samples is None:
+            self.samples = new
+        else:
+            self.samples = {k: np.concatenate([self.samples[k], new[k]]) for k in new}
 
     @property
     def w_hat(self) -> torch.Tensor:
@@ -159,9 +185,12 @@ class EmulatorModel:
         return {k: v[idx] for k, v in self.samples.items()}
 
     def save_model_info(self, path):
-        """Samples + current parameters as ``path + '.npz'`` (plain arrays, no pickle)."""
+        """Samples, current values and step sizes as ``path + '.npz'`` (plain arrays)."""
         arrs = {f"samples_{k}": v for k, v in (self.samples or {}).items()}
-        arrs.update({f"param_{k}": v for k, v in self.params.items()})
+        for k in ModelParams.names:
+            p = getattr(self.params, k)
+            arrs[f"param_{k}"] = p.val
+            arrs[f"step_{k}"] = p.mcmcStepParam
         np.savez(path if path.endswith(".npz") else path + ".npz", **arrs)
 
     def restore_model_info(self, path):
@@ -171,6 +200,9 @@ class EmulatorModel:
             for k in z.files:
                 if k.startswith("param_"):
                     self.params[k[6:]] = z[k]
+                elif k.startswith("step_"):
+                    p = getattr(self.params, k[5:])
+                    p.mcmcStepParam = np.broadcast_to(z[k], p.val_shape).copy()
         self.samples = samples or None
 
     # ------------------------------------------------------------------------- likelihood
@@ -180,7 +212,7 @@ class EmulatorModel:
         Building block of SEPIA's logLik for the sim-only model (driven by do_mcmc,
         src/model.py:234-235): one batched Gram -> Cholesky -> nll over the P GPs.
         """
-        pr = self.params if params is None else params
+        pr = self.params.values() if params is None else params
         samples = {k: np.asarray(pr[k]).reshape(1, -1) for k in self.param_names}
         beta, s, delta, _ = gp_params(samples, _np(self.LamSim), self.d, self.P, False)
         X = self.data.sim_data.t

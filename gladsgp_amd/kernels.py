@@ -201,6 +201,38 @@ def nll(chol: Cholesky, w) -> torch.Tensor:
     return out
 
 
+class LoglikWorkspace:
+    """Device scratch of :func:`loglik` for fixed (n, batch): allocated once, so a Metropolis
+    sweep calls gp_loglik with no allocation and no host synchronisation."""
+
+    def __init__(self, n: int, batch: int, device):
+        self.n, self.batch = n, batch
+        nbytes = int(_capi.lib().gp_loglik_ws_bytes(n, batch))
+        self.buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        self.info = torch.zeros(batch, dtype=torch.int32, device=device)
+
+
+def loglik(X: torch.Tensor, beta: torch.Tensor, s: torch.Tensor, delta: torch.Tensor,
+           w: torch.Tensor, ws: LoglikWorkspace, out: torch.Tensor | None = None) -> torch.Tensor:
+    """ll[b] = -(1/2 w_b^T G_b^-1 w_b + 1/2 log|G_b|), G_b = s_b exp(-sum beta_b (dx)^2) + delta_b I;
+    -inf where G_b is not positive definite (gp_loglik: Gram -> Cholesky -> quadratic form).
+
+    X (n, d); beta (batch, d); s, delta (batch,); w (batch, n) -- all float64 on the device.
+    """
+    n, d = X.shape
+    batch = ws.batch
+    if n != ws.n or beta.shape != (batch, d) or w.shape != (batch, n):
+        raise ValueError("loglik: shapes do not match the workspace")
+    for t, nm in ((X, "X"), (beta, "beta"), (s, "s"), (delta, "delta"), (w, "w")):
+        if t.dtype != F64 or not t.is_contiguous():
+            raise TypeError(f"{nm} must be contiguous float64")
+    out = torch.empty(batch, dtype=F64, device=X.device) if out is None else out
+    _capi.call("gp_loglik", X.data_ptr(), n, d, d, beta.data_ptr(), d, s.data_ptr(),
+               delta.data_ptr(), w.data_ptr(), n, batch, ws.buf.data_ptr(), ws.buf.numel(),
+               out.data_ptr(), ws.info.data_ptr(), _stream(X.device))
+    return out
+
+
 def trmv(chol: Cholesky, w) -> torch.Tensor:
     """z = L^-1 w per problem -> (batch, n)."""
     dev = chol.linv_buf.device

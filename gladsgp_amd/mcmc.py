@@ -1,0 +1,385 @@
+"""Metropolis fit of the sim-only GPMSA emulator on the GPU (SEPIA's do_mcmc / tune_step_sizes).
+
+Reference usage replaced (``src/model.py:218-238``)::
+
+    model.params.lamWOs = SepiaParam(val=pc_prec, name='lamWOs', val_shape=(1, 1),
+        dist='Gamma', params=[50, 50/pc_prec], bounds=[1., np.inf], mcmcStepParam=10,
+        mcmcStepType='Uniform')
+    model.params.mcmcList = [model.params.betaU, model.params.lamUz, model.params.lamWs,
+                             model.params.lamWOs]
+    model.tune_step_sizes(100, 5)
+    model.do_mcmc(512)
+
+SEPIA (``timghill/SEPIA@ffe3b60``) is not available offline, so the
+sampler is restated from the GPMSA model it implements; every constant below that the
+reference's own files do not pin is marked *unpinned*.
+
+Model (per principal component j = 0..P-1, one GP each, w_hat_j = PC weights of the n runs)::
+
+    Sigma_j = (1/lamUz_j) exp(-sum_k betaU[k+1, j] (t_ik - t_i'k)^2)
+              + (1/lamWs_j + 1/(lamWOs LamSim_j)) I
+    loglik  = sum_j  -1/2 log|Sigma_j| - 1/2 w_hat_j^T Sigma_j^-1 w_hat_j           
+
+betaU is (d+1, P); row 0 belongs to the dummy x input, whose differences are all zero, so it
+only moves under its prior (the reference's sample layout ``(S, (d+1) P)``, C order,
+``mcmc_diagnostics_advanced.py:57``).
+
+Priors (log densities up to constants) and proposals:
+
+  ===========  ===================================  ==========  ===========  ============
+  param        prior                                bounds      step (dflt)  step type
+  ===========  ===================================  ==========  ===========  ============
+  betaU        Beta(1, 0.1) on rho = exp(-beta/4)   [0, inf)    0.1          BetaRho
+  lamUz        Gamma(5, 5)                          [0.3, inf)  5            Uniform
+  lamWs        Gamma(3, 0.003)                      [60, 1e5]   100          Uniform
+  lamWOs       Gamma(5, 0.005); the reference       [60, 1e5]   100          Uniform
+               overrides it with Gamma(50, 50/pc_prec), [1, inf), step 10 (model.py:225-229)
+  ===========  ===================================  ==========  ===========  ============
+
+The default step sizes are pinned by ``examples/03...ipynb:192-208``; the prior families,
+parameters and bounds are the GPMSA defaults and are *unpinned*.  Gamma is (shape, rate).
+Proposals: ``Uniform`` x' = x + step (u - 1/2); ``BetaRho`` the same move on rho, then
+beta' = -4 log rho'.  A proposal outside the bounds is rejected.  Acceptance:
+log u < log post(x') - log post(x).
+
+Sweep (one MCMC iteration) = component-wise Metropolis over mcmcList in order: betaU row by
+row, then lamUz, lamWs, lamWOs.  Given lamWOs the P GPs are independent, so the P elements of
+one betaU row (or of lamUz, lamWs) are proposed together and accepted or rejected one by one:
+that is the same Markov kernel as updating them one after another, evaluated as ONE batched
+gp_loglik (Gram -> Cholesky -> quadratic form for the P GPs).  lamWOs touches every GP and is
+accepted on the sum.  The whole sweep is stream-ordered device work: no host synchronisation,
+proposals and accept/reject are device tensor ops on uniforms drawn on the host from a seeded
+numpy Generator (so a CPU restatement fed the same uniforms reproduces the chain).
+
+tune_step_sizes(n_burn, n_levels): for each level l the steps are default * 2^e_l, e_l evenly
+spaced in [-(n_levels-1)/2, (n_levels-1)/2]; n_burn sweeps are run at each level continuing the
+chain, acceptances are counted per element, and a binomial logistic regression of acceptance on
+log(step) gives the step whose predicted acceptance is 1/e (logit = log(1/(e-1))).  Ladder base,
+target and the pseudo-count regularisation are *unpinned* (GPMSA's stepsize procedure).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import kernels
+
+F64 = torch.float64
+TARGET_LOGIT = math.log(1.0 / (math.e - 1.0))   # acceptance 1/e
+RHO_MAX = 0.999                                  # rho clipped in the Beta prior (beta -> 0)
+
+
+class SepiaParam:
+    """One model parameter: value, prior and Metropolis step (SEPIA's SepiaParam surface).
+
+    Signature as the reference calls it (``src/model.py:225-229``).
+    """
+
+    def __init__(self, val, name, val_shape, dist="Normal", params=None, bounds=None,
+                 mcmcStepParam=0.1, mcmcStepType="Uniform", fixed=None):
+        self.name = name
+        self.val_shape = tuple(val_shape)
+        self.val = np.broadcast_to(np.asarray(val, dtype=np.float64), self.val_shape).copy()
+        if dist not in ("Gamma", "Beta", "Uniform", "Normal"):
+            raise ValueError(f"unsupported prior {dist!r}")
+        self.dist = dist
+        self.params = [float(p) for p in (params if params is not None else [0.0, 1.0])]
+        b = bounds if bounds is not None else [-np.inf, np.inf]
+        self.bounds = (float(b[0]), float(b[1]))
+        self.mcmcStepParam = np.broadcast_to(np.asarray(mcmcStepParam, dtype=np.float64),
+                                             self.val_shape).copy()
+        if mcmcStepType not in ("Uniform", "BetaRho"):
+            raise ValueError(f"unsupported step type {mcmcStepType!r}")
+        self.mcmcStepType = mcmcStepType
+        self.fixed = np.zeros(self.val_shape, bool) if fixed is None else np.asarray(fixed, bool)
+
+    def __repr__(self):
+        return (f"SepiaParam({self.name}, shape={self.val_shape}, {self.dist}{self.params}, "
+                f"bounds={self.bounds}, step={self.mcmcStepType})")
+
+
+class ModelParams:
+    """``model.params``: attributes betaU, lamUz, lamWs, lamWOs and ``mcmcList``."""
+
+    names = ("betaU", "lamUz", "lamWs", "lamWOs")
+
+    def __init__(self, d: int, P: int):
+        # GPMSA / SEPIA defaults (step sizes pinned by 03...ipynb:192-208; the rest unpinned)
+        self.betaU = SepiaParam(0.1, "betaU", (d + 1, P), "Beta", [1.0, 0.1], [0.0, np.inf],
+                                0.1, "BetaRho")
+        self.lamUz = SepiaParam(1.0, "lamUz", (1, P), "Gamma", [5.0, 5.0], [0.3, np.inf],
+                                5.0, "Uniform")
+        self.lamWs = SepiaParam(1000.0, "lamWs", (1, P), "Gamma", [3.0, 0.003], [60.0, 1e5],
+                                100.0, "Uniform")
+        self.lamWOs = SepiaParam(1000.0, "lamWOs", (1, 1), "Gamma", [5.0, 0.005], [60.0, 1e5],
+                                 100.0, "Uniform")
+        self.mcmcList = [self.betaU, self.lamUz, self.lamWs, self.lamWOs]
+
+    def __getitem__(self, name):          # dict-style access to values
+        return getattr(self, name).val
+
+    def __setitem__(self, name, value):
+        p = getattr(self, name)
+        p.val = np.broadcast_to(np.asarray(value, dtype=np.float64), p.val_shape).copy()
+
+    def values(self) -> dict:
+        return {k: getattr(self, k).val.copy() for k in self.names}
+
+
+# ------------------------------------------------------------------------------ priors (torch)
+def log_prior(p: SepiaParam, x: torch.Tensor) -> torch.Tensor:
+    """Elementwise log prior density of parameter ``p`` at values ``x`` (device tensor)."""
+    a, b = p.params
+    if p.dist == "Gamma":
+        return (a - 1.0) * torch.log(x) - b * x
+    if p.dist == "Beta":                    # on rho = exp(-x / 4)
+        rho = torch.clamp(torch.exp(-x / 4.0), max=RHO_MAX)
+        return (a - 1.0) * torch.log(rho) + (b - 1.0) * torch.log1p(-rho)
+    if p.dist == "Normal":
+        return -0.5 * ((x - a) / b) ** 2
+    return torch.zeros_like(x)              # Uniform on the bounds
+
+
+def propose(p: SepiaParam, x: torch.Tensor, step: torch.Tensor, u: torch.Tensor):
+    """Candidate values and in-bounds mask for a Metropolis move of ``p``."""
+    if p.mcmcStepType == "BetaRho":
+        rho = torch.exp(-x / 4.0) + step * (u - 0.5)
+        ok = (rho > 0.0) & (rho <= 1.0)
+        cand = -4.0 * torch.log(torch.where(ok, rho, torch.ones_like(rho)))
+    else:
+        cand = x + step * (u - 0.5)
+        ok = torch.ones_like(cand, dtype=torch.bool)
+    lo, hi = p.bounds
+    ok = ok & (cand >= lo) & (cand <= hi)
+    return torch.where(ok, cand, x), ok
+
+
+# --------------------------------------------------------------------------- device sampler
+@dataclass
+class ChainState:
+    betaU: torch.Tensor        # (d+1, P)
+    lamUz: torch.Tensor        # (P,)
+    lamWs: torch.Tensor        # (P,)
+    lamWOs: torch.Tensor       # (1,)
+    ll: torch.Tensor           # (P,) current per-GP log-likelihood
+    acc: dict = field(default_factory=dict)   # per-parameter acceptance counters (device)
+
+
+def uniforms_per_sweep(d: int, P: int) -> int:
+    """Uniform draws one sweep consumes: (proposal, acceptance) per updated element."""
+    return 2 * ((d + 1) * P + 2 * P + 1)
+
+
+class GPUSampler:
+    """Component-wise Metropolis over the P PC-GPs of one emulator, all state on the device."""
+
+    def __init__(self, X: torch.Tensor, w_hat: torch.Tensor, LamSim: torch.Tensor,
+                 params: ModelParams):
+        self.X = X.contiguous()
+        self.w = w_hat.contiguous()                 # (P, n)
+        self.P, self.n = self.w.shape
+        self.d = self.X.shape[1]
+        self.dev = self.X.device
+        self.lam = LamSim.to(self.dev, F64).reshape(self.P).contiguous()
+        self.params = params
+        self.ws = kernels.LoglikWorkspace(self.n, self.P, self.dev)
+        self._beta = torch.empty((self.P, self.d), dtype=F64, device=self.dev)
+        self._s = torch.empty(self.P, dtype=F64, device=self.dev)
+        self._delta = torch.empty(self.P, dtype=F64, device=self.dev)
+        self._ll = torch.empty(self.P, dtype=F64, device=self.dev)
+
+    def _t(self, a) -> torch.Tensor:
+        return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=self.dev)
+
+    def state_from_params(self) -> ChainState:
+        pr = self.params
+        st = ChainState(self._t(pr.betaU.val), self._t(pr.lamUz.val).reshape(self.P),
+                        self._t(pr.lamWs.val).reshape(self.P), self._t(pr.lamWOs.val).reshape(1),
+                        torch.empty(self.P, dtype=F64, device=self.dev))
+        st.ll = self.loglik(st.betaU, st.lamUz, st.lamWs, st.lamWOs).clone()
+        return st
+
+    def loglik(self, betaU, lamUz, lamWs, lamWOs) -> torch.Tensor:
+        """Per-GP log-likelihood (P,) for the given parameters (one gp_loglik call)."""
+        self._beta.copy_(betaU[1:].transpose(0, 1))
+        torch.reciprocal(lamUz, out=self._s)
+        torch.add(torch.reciprocal(lamWs), torch.reciprocal(lamWOs * self.lam), out=self._delta)
+        return kernels.loglik(self.X, self._beta, self._s, self._delta, self.w, self.ws,
+                              out=self._ll)
+
+    def log_post(self, st: ChainState) -> torch.Tensor:
+        pr = self.params
+        lp = st.ll.sum()
+        lp = lp + log_prior(pr.betaU, st.betaU).sum() + log_prior(pr.lamUz, st.lamUz).sum()
+        lp = lp + log_prior(pr.lamWs, st.lamWs).sum() + log_prior(pr.lamWOs, st.lamWOs).sum()
+        return lp
+
+    def sweep(self, st: ChainState, u: torch.Tensor, steps: dict) -> None:
+        """One component-wise Metropolis sweep; ``u`` holds uniforms_per_sweep uniforms."""
+        pr, P, d = self.params, self.P, self.d
+        o = 0
+
+        def take(k):
+            nonlocal o
+            r = u[o:o + k]
+            o += k
+            return r
+
+        def count(name, acc):
+            c = st.acc.get(name)
+            if c is None:
+                st.acc[name] = acc.to(F64)
+            else:
+                c.add_(acc.to(F64))
+
+        # betaU, one row (all P GPs) at a time
+        for k in range(d + 1):
+            up, ua = take(P), take(P)
+            cur = st.betaU[k]
+            cand, ok = propose(pr.betaU, cur, steps["betaU"][k], up)
+            dlp = log_prior(pr.betaU, cand) - log_prior(pr.betaU, cur)
+            if k == 0:                       # dummy x: the likelihood does not depend on it
+                acc = ok & (torch.log(ua) < dlp)
+                st.betaU[0] = torch.where(acc, cand, cur)
+            else:
+                trial = st.betaU.clone()
+                trial[k] = cand
+                ll_new = self.loglik(trial, st.lamUz, st.lamWs, st.lamWOs)
+                acc = ok & (torch.log(ua) < ll_new - st.ll + dlp)
+                st.betaU[k] = torch.where(acc, cand, cur)
+                st.ll = torch.where(acc, ll_new, st.ll)
+            count(("betaU", k), acc)
+        # lamUz, lamWs: all P GPs at once
+        for name in ("lamUz", "lamWs"):
+            up, ua = take(P), take(P)
+            cur = getattr(st, name)
+            p = getattr(pr, name)
+            cand, ok = propose(p, cur, steps[name].reshape(P), up)
+            args = {"lamUz": st.lamUz, "lamWs": st.lamWs}
+            args[name] = cand
+            ll_new = self.loglik(st.betaU, args["lamUz"], args["lamWs"], st.lamWOs)
+            acc = ok & (torch.log(ua) < ll_new - st.ll + log_prior(p, cand) - log_prior(p, cur))
+            setattr(st, name, torch.where(acc, cand, cur))
+            st.ll = torch.where(acc, ll_new, st.ll)
+            count(name, acc)
+        # lamWOs: shared by every GP, accepted on the sum
+        up, ua = take(1), take(1)
+        p = pr.lamWOs
+        cur = st.lamWOs
+        cand, ok = propose(p, cur, steps["lamWOs"].reshape(1), up)
+        ll_new = self.loglik(st.betaU, st.lamUz, st.lamWs, cand)
+        dl = (ll_new - st.ll).sum() + (log_prior(p, cand) - log_prior(p, cur)).sum()
+        acc = ok & (torch.log(ua) < dl)
+        st.lamWOs = torch.where(acc, cand, cur)
+        st.ll = torch.where(acc, ll_new, st.ll)
+        count("lamWOs", acc)
+
+    def steps_tensor(self, scale: float = 1.0) -> dict:
+        pr = self.params
+        return {"betaU": self._t(pr.betaU.mcmcStepParam * scale),
+                "lamUz": self._t(pr.lamUz.mcmcStepParam * scale),
+                "lamWs": self._t(pr.lamWs.mcmcStepParam * scale),
+                "lamWOs": self._t(pr.lamWOs.mcmcStepParam * scale)}
+
+    def write_back(self, st: ChainState) -> None:
+        pr = self.params
+        pr.betaU.val = st.betaU.cpu().numpy().reshape(pr.betaU.val_shape)
+        pr.lamUz.val = st.lamUz.cpu().numpy().reshape(pr.lamUz.val_shape)
+        pr.lamWs.val = st.lamWs.cpu().numpy().reshape(pr.lamWs.val_shape)
+        pr.lamWOs.val = st.lamWOs.cpu().numpy().reshape(pr.lamWOs.val_shape)
+
+    def run(self, nsamp: int, rng: np.random.Generator, steps: dict | None = None,
+            st: ChainState | None = None, record: bool = True, block: int = 64):
+        """``nsamp`` sweeps; returns (state, samples dict of numpy arrays or None)."""
+        st = self.state_from_params() if st is None else st
+        steps = self.steps_tensor() if steps is None else steps
+        nu = uniforms_per_sweep(self.d, self.P)
+        P, d = self.P, self.d
+        if record:
+            rec = {"betaU": torch.empty((nsamp, (d + 1) * P), dtype=F64, device=self.dev),
+                   "lamUz": torch.empty((nsamp, P), dtype=F64, device=self.dev),
+                   "lamWs": torch.empty((nsamp, P), dtype=F64, device=self.dev),
+                   "lamWOs": torch.empty((nsamp, 1), dtype=F64, device=self.dev),
+                   "logPost": torch.empty((nsamp, 1), dtype=F64, device=self.dev)}
+        for a in range(0, nsamp, block):
+            b = min(nsamp, a + block)
+            U = self._t(rng.random((b - a, nu)))
+            for i in range(a, b):
+                self.sweep(st, U[i - a], steps)
+                if record:
+                    rec["betaU"][i] = st.betaU.reshape(-1)
+                    rec["lamUz"][i] = st.lamUz
+                    rec["lamWs"][i] = st.lamWs
+                    rec["lamWOs"][i] = st.lamWOs
+                    rec["logPost"][i] = self.log_post(st)
+        samples = {k: v.cpu().numpy() for k, v in rec.items()} if record else None
+        return st, samples
+
+
+# --------------------------------------------------------------------------- step tuning
+def logistic_step(log_steps: np.ndarray, accepts: np.ndarray, trials: int,
+                  target_logit: float = TARGET_LOGIT, pseudo: float = 0.5) -> float:
+    """Step whose fitted acceptance probability hits the target (binomial logit regression of
+    acceptance on log step, IRLS; ``pseudo`` successes/failures per level keep the fit finite
+    when a level accepts everything or nothing).  Returns exp(log step*)."""
+    x = np.asarray(log_steps, dtype=np.float64)
+    yk = np.asarray(accepts, dtype=np.float64) + pseudo
+    nk = float(trials) + 2.0 * pseudo
+    A = np.stack([np.ones_like(x), x], axis=1)
+    bvec = np.zeros(2)
+    for _ in range(50):
+        eta = A @ bvec
+        p = 1.0 / (1.0 + np.exp(-eta))
+        wgt = nk * p * (1.0 - p)
+        grad = A.T @ (yk - nk * p)
+        H = A.T @ (A * wgt[:, None])
+        try:
+            dlt = np.linalg.solve(H, grad)
+        except np.linalg.LinAlgError:
+            break
+        bvec = bvec + dlt
+        if np.max(np.abs(dlt)) < 1e-10:
+            break
+    b0, b1 = bvec
+    rate = yk / nk
+    if not np.isfinite(b1) or b1 >= -1e-12:
+        # acceptance should fall as the step grows; otherwise take the closest level
+        return float(np.exp(x[int(np.argmin(np.abs(rate - 1.0 / math.e)))]))
+    return float(np.exp((target_logit - b0) / b1))
+
+
+def tune_step_sizes(sampler: GPUSampler, n_burn: int, n_levels: int,
+                    rng: np.random.Generator, st: ChainState | None = None) -> ChainState:
+    """GPMSA-style step-size tuning (see module doc); updates params' mcmcStepParam in place
+    and returns the chain state reached."""
+    pr = sampler.params
+    st = sampler.state_from_params() if st is None else st
+    ex = np.linspace(-(n_levels - 1) / 2.0, (n_levels - 1) / 2.0, n_levels)
+    base = {k: getattr(pr, k).mcmcStepParam.copy() for k in ModelParams.names}
+    counts = []
+    for e in ex:
+        scale = 2.0 ** e
+        st.acc = {}
+        st, _ = sampler.run(n_burn, rng, steps=sampler.steps_tensor(scale), st=st, record=False)
+        counts.append({k: v.cpu().numpy() for k, v in st.acc.items()})
+    logs = {k: np.log(base[k][None] * (2.0 ** ex).reshape((-1,) + (1,) * base[k].ndim))
+            for k in base}
+    P, d = sampler.P, sampler.d
+    new = {k: base[k].copy() for k in base}
+    for k in range(d + 1):
+        for j in range(P):
+            acc = np.array([c[("betaU", k)][j] for c in counts])
+            new["betaU"][k, j] = logistic_step(logs["betaU"][:, k, j], acc, n_burn)
+    for name in ("lamUz", "lamWs"):
+        for j in range(P):
+            acc = np.array([c[name][j] for c in counts])
+            new[name][0, j] = logistic_step(logs[name][:, 0, j], acc, n_burn)
+    acc = np.array([c["lamWOs"][0] for c in counts])
+    new["lamWOs"][0, 0] = logistic_step(logs["lamWOs"][:, 0, 0], acc, n_burn)
+    for k in base:
+        getattr(pr, k).mcmcStepParam = new[k]
+    st.acc = {}
+    return st

@@ -9,9 +9,8 @@ every array operation on the GPU through libgpfit:
     ``create_K_basis(K.astype(np.float32))``                           (model.py:100-102, A3)
   * PC weights / LamSim of the SEPIA model and the truncation precision ``pc_prec`` with the
     ``lamWOs ~ Gamma(50, 50/pc_prec)`` prior                            (model.py:218-229, A4)
-``fit_models`` needs the Metropolis MCMC of SEPIA (``tune_step_sizes`` / ``do_mcmc``,
-model.py:234-235) which is the next component on the path: this round it
-prepares everything up to the sampler and raises ``NotImplementedError`` at that point.
+``fit_models`` then runs SEPIA's Metropolis fit (``tune_step_sizes`` / ``do_mcmc``,
+model.py:234-235) on the GPU (gladsgp_amd.mcmc) and saves models + ``timing.csv``.
 """
 from __future__ import annotations
 
@@ -24,6 +23,7 @@ import torch
 from . import blas
 from .blas import CM, gemm
 from .emulator import EmulatorData, EmulatorModel
+from .mcmc import SepiaParam
 from .svd import randomized_svd
 
 PMAX = 25   # model.py:81
@@ -110,17 +110,22 @@ def load_model(train_config, m, p, dtype=np.float32, device=None):
     return data, model
 
 
-def fit_models(train_config, n_sims, n_pcs, dtype=np.float32, recompute=False, device=None):
-    """src/model.py:152-245 up to the sampler: PCA timing, pc_prec and the lamWOs prior.
-
-    The Metropolis MCMC (``tune_step_sizes(100, 5)``; ``do_mcmc(512)``) is the next component
-    on the path and is not part of this build yet.
+def fit_models(train_config, n_sims, n_pcs, dtype=np.float32, recompute=False, device=None,
+               n_burn=100, n_levels=5, nsamp=512, seed=None):
+    """src/model.py:152-245: for every (m, p), PCA + standardisation (init_model), the
+    truncation precision pc_prec and its lamWOs prior Gamma(50, 50/pc_prec) with bounds
+    [1, inf), start pc_prec, Uniform step 10 (model.py:218-231); then
+    ``tune_step_sizes(100, 5)`` and ``do_mcmc(512)`` (model.py:234-235) on the GPU; saves
+    each model and ``timing.csv`` (sims, PCs, PCA seconds, MCMC seconds) like the reference.
+    ``n_burn``/``n_levels``/``nsamp`` default to the reference's values; ``seed`` seeds the
+    sampler's uniforms (the reference uses numpy's global state).
     """
     t_std = np.loadtxt(train_config.X_standard, delimiter=",", skiprows=1,
                        comments=None).astype(dtype)
     y_sim = np.load(train_config.Y_physical).T.astype(dtype)
     data_dir = os.path.join(train_config.data_dir, "models")
     os.makedirs(data_dir, exist_ok=True)
+    models, rows = [], []
     for m in n_sims:
         for p in n_pcs:
             t0 = time.perf_counter()
@@ -128,11 +133,28 @@ def fit_models(train_config, n_sims, n_pcs, dtype=np.float32, recompute=False, d
                                      exp="{}_n{:03d}".format(train_config.exp, m), p=p,
                                      data_dir=data_dir, recompute=recompute, device=device)
             torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
+            dt_pca = time.perf_counter() - t0
             prec = pc_precision(data)
-            print("PC PRECISION:", prec, "PCA seconds:", dt)
-            model.lamWOs_prior = {"dist": "Gamma", "params": [50.0, 50.0 / prec],
-                                  "start": prec, "bounds": [1.0, np.inf], "step": 10.0}
-            raise NotImplementedError(
-                "fit_models: SEPIA's Metropolis MCMC (tune_step_sizes/do_mcmc) is the next "
-                "component of this build (SURVEY §8f rank 2); use load_model with saved samples")
+            print("PC PRECISION:", prec)
+            gamma_a = 50.0
+            model.params.lamWOs = SepiaParam(val=prec, name="lamWOs", val_shape=(1, 1),
+                                             dist="Gamma", params=[gamma_a, gamma_a / prec],
+                                             bounds=[1.0, np.inf], mcmcStepParam=10,
+                                             mcmcStepType="Uniform")
+            model.params.mcmcList = [model.params.betaU, model.params.lamUz,
+                                     model.params.lamWs, model.params.lamWOs]
+            if seed is not None:
+                model.rng = np.random.default_rng(seed)
+            t0 = time.perf_counter()
+            model.tune_step_sizes(n_burn, n_levels)
+            model.do_mcmc(nsamp)
+            torch.cuda.synchronize()
+            dt_mcmc = time.perf_counter() - t0
+            model.save_model_info(os.path.join(data_dir,
+                                               "{}_n{:03d}_p{:02d}".format(train_config.exp,
+                                                                           m, p)))
+            models.append(model)
+            rows.append([m, p, dt_pca, dt_mcmc])
+    np.savetxt(os.path.join(data_dir, "timing.csv"), np.array(rows, dtype=np.float64),
+               delimiter=",", fmt="%.3f", header="sims,PCs,PCA (seconds),MCMC (seconds)")
+    return models

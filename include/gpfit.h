@@ -134,6 +134,20 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
            const double* w, int ldw, const double* logdet, double* nll, double* work,
            int batch, hipStream_t stream);
 
+/*
+ * Batched GP log-likelihood in one stream-ordered call: Gram (gp_gram_ardse) -> Cholesky
+ * (gp_potrf_inv) -> ll[b] = -(1/2 ||L_b^-1 w_b||^2 + 1/2 log|G_b|), no 2*pi term, with
+ * ll[b] = -inf where the factorisation failed (info[b] != 0, optionally copied out to `info`).
+ * `ws` is caller-owned device scratch of gp_loglik_ws_bytes(n, batch) bytes.  Never syncs,
+ * so a Metropolis sweep can be stream-ordered (and graph-captured) end to end.
+ * Replaces the per-PC term of SEPIA's logLik evaluated by SepiaModel.do_mcmc /
+ * tune_step_sizes (src/model.py:234-235): Sigma_j = s_j R(beta_j) + delta_j I, w = w_hat_j.
+ */
+long long gp_loglik_ws_bytes(int n, int batch);
+int gp_loglik(const double* X, int n, int d, int ldx, const double* beta, int ldbeta,
+              const double* s, const double* delta, const double* w, int ldw, int batch,
+              void* ws, long long ws_bytes, double* ll, int* info, hipStream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Fit-side dense kernels (src/model.py init_model and src/svd.py randomized_svd).
  * ---------------------------------------------------------------------------------------- */

@@ -1,0 +1,137 @@
+"""GPU Metropolis fit (gladsgp_amd.mcmc, gp_loglik) against the oracle restatement
+(oracle/mcmc_ref.py) fed the same uniforms, and the fit_models -> load_model round trip."""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from gladsgp_amd import kernels, mcmc
+from oracle import gp_ref, mcmc_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+def _t(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)
+
+
+def _problem(n, d, P, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.random((n, d))
+    lam = rng.uniform(1.0, 10.0, P)
+    w = np.empty((P, n))
+    for j in range(P):   # PC weights drawn from a GP so the chain has structure to find
+        G = gp_ref.gram_ardse(X, rng.uniform(0.5, 4.0, d), 1.0, 1e-3)
+        w[j] = np.linalg.cholesky(G) @ rng.standard_normal(n)
+    return X, w, lam
+
+
+@pytest.mark.parametrize("n,P", [(64, 3), (200, 5), (257, 2)])
+def test_loglik_matches_oracle(dev, n, P):
+    d = 4
+    X, w, lam = _problem(n, d, P, seed=n)
+    rng = np.random.default_rng(7)
+    betaU = rng.uniform(0.2, 5.0, (d + 1, P))
+    lamUz = rng.uniform(0.5, 3.0, P)
+    lamWs = rng.uniform(100, 5000, P)
+    lamWOs = 300.0
+    ref = mcmc_ref.loglik_pcs(X, w, lam, betaU, lamUz, lamWs, lamWOs)
+    ws = kernels.LoglikWorkspace(n, P, dev)
+    beta = _t(betaU[1:].T, dev)
+    s = _t(1.0 / lamUz, dev)
+    delta = _t(1.0 / lamWs + 1.0 / (lamWOs * lam), dev)
+    got = kernels.loglik(_t(X, dev), beta, s, delta, _t(w, dev), ws).cpu().numpy()
+    tol = 1e-9 * np.maximum(1.0, np.abs(ref))
+    assert np.all(np.abs(got - ref) <= tol), (got, ref)
+    assert np.all(ws.info.cpu().numpy() == 0)
+
+
+def test_loglik_non_pd_is_minus_inf(dev):
+    n, d, P = 96, 2, 3
+    X, w, lam = _problem(n, d, P, seed=3)
+    beta = _t(np.full((P, d), 0.5), dev)
+    s = _t([1.0, 1.0, 1.0], dev)
+    delta = _t([1e-3, -5.0, 1e-3], dev)         # problem 1 is indefinite
+    ws = kernels.LoglikWorkspace(n, P, dev)
+    got = kernels.loglik(_t(X, dev), beta, s, delta, _t(w, dev), ws).cpu().numpy()
+    assert np.isfinite(got[0]) and np.isfinite(got[2]) and got[1] == -np.inf
+    assert ws.info.cpu().numpy()[1] > 0
+
+
+def _spec(pr):
+    return {k: (getattr(pr, k).dist, getattr(pr, k).params, getattr(pr, k).bounds,
+                getattr(pr, k).mcmcStepType) for k in pr.names}
+
+
+@pytest.mark.parametrize("n,d,P,steps_scale", [(48, 2, 3, 1.0), (130, 3, 2, 0.3)])
+def test_chain_matches_oracle(dev, n, d, P, steps_scale):
+    X, w, lam = _problem(n, d, P, seed=11 + n)
+    pr = mcmc.ModelParams(d, P)
+    for k in pr.names:
+        getattr(pr, k).mcmcStepParam = getattr(pr, k).mcmcStepParam * steps_scale
+    sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr)
+    nsw = 25
+    st, rec = sampler.run(nsw, np.random.default_rng(5))
+    U = np.random.default_rng(5).random((nsw, mcmc.uniforms_per_sweep(d, P)))
+    state = {"betaU": pr.betaU.val, "lamUz": pr.lamUz.val[0], "lamWs": pr.lamWs.val[0],
+             "lamWOs": pr.lamWOs.val[0, 0]}
+    steps = {k: getattr(pr, k).mcmcStepParam for k in pr.names}
+    _, ref, acc = mcmc_ref.run_chain(X, w, lam, _spec(pr), state, steps, U)
+    for k in ("betaU", "lamUz", "lamWs", "lamWOs"):
+        np.testing.assert_allclose(rec[k], ref[k], rtol=1e-9, atol=1e-12, err_msg=k)
+    assert acc["betaU"][1:].sum() > 0            # the chain actually moved
+    assert np.all(np.isfinite(rec["logPost"]))
+
+
+def test_tune_and_sample(dev):
+    n, d, P = 80, 3, 2
+    X, w, lam = _problem(n, d, P, seed=21)
+    pr = mcmc.ModelParams(d, P)
+    sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr)
+    rng = np.random.default_rng(0)
+    st = mcmc.tune_step_sizes(sampler, 20, 3, rng)
+    for k in pr.names:
+        stp = getattr(pr, k).mcmcStepParam
+        assert np.all(np.isfinite(stp)) and np.all(stp > 0), k
+    st, rec = sampler.run(40, rng, st=st)
+    assert rec["betaU"].shape == (40, (d + 1) * P)
+    assert np.all(np.isfinite(rec["logPost"]))
+
+
+def test_fit_models_roundtrip(dev, tmp_path):
+    from gladsgp_amd import model as gmodel
+    from gladsgp_amd.emulator import SepiaEmulatorPrediction
+    rng = np.random.default_rng(4)
+    n, ny, d = 40, 300, 3
+    t = rng.random((n, d))
+    modes = rng.standard_normal((4, ny))
+    y = np.stack([np.sin(2 * np.pi * t @ rng.uniform(0, 1, d) + k) for k in range(4)], 1) @ modes
+    y = y + 1e-2 * rng.standard_normal((n, ny))
+    xcsv = tmp_path / "X_std.csv"
+    np.savetxt(xcsv, t, delimiter=",", header=",".join(f"x{i}" for i in range(d)), comments="")
+    ynpy = tmp_path / "Y.npy"
+    np.save(ynpy, y.T)                           # the reference stores (ny, n)
+    cfg = types.SimpleNamespace(X_standard=str(xcsv), Y_physical=str(ynpy),
+                                data_dir=str(tmp_path), exp="toy")
+    models = gmodel.fit_models(cfg, [n], [3], dtype=np.float64, device=dev, n_burn=10,
+                               n_levels=3, nsamp=16, seed=1)
+    assert len(models) == 1
+    assert models[0].samples["lamUz"].shape == (16, 3)
+    tim = np.loadtxt(tmp_path / "models" / "timing.csv", delimiter=",")
+    assert tim.shape == (4,) and tim[0] == n and tim[1] == 3
+    data, mdl = gmodel.load_model(cfg, n, 3, dtype=np.float64, device=dev)
+    np.testing.assert_array_equal(mdl.samples["betaU"], models[0].samples["betaU"])
+    np.testing.assert_array_equal(mdl.params.lamWs.mcmcStepParam,
+                                  models[0].params.lamWs.mcmcStepParam)
+    samples = mdl.get_samples(numsamples=4, nburn=4)
+    pred = SepiaEmulatorPrediction(model=mdl, samples=samples, t_pred=rng.random((7, d)))
+    assert pred.w.shape == (4, 7, 3) and np.all(np.isfinite(pred.var))
+    assert pred.get_y().shape == (4, 7, ny)
