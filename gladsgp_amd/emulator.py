@@ -136,7 +136,6 @@ class EmulatorModel:
         self.params = ModelParams(self.d, self.P)
         self.samples = None
         self.rng = np.random.default_rng()
-        self._chain = None            # device chain state carried from tuning into sampling
 
     # ---------------------------------------------------------------------------- sampling
     def _sampler(self) -> mcmc.GPUSampler:
@@ -148,18 +147,22 @@ class EmulatorModel:
         """SEPIA tune_step_sizes (src/model.py:234): per-element Metropolis step sizes from
         n_levels x n_burn sweeps on the GPU (algorithm: gladsgp_amd.mcmc module doc)."""
         sm = self._sampler()
-        st = mcmc.tune_step_sizes(sm, int(n_burn), int(n_levels), self.rng)
+        mcmc.tune_step_sizes(sm, int(n_burn), int(n_levels), self.rng)
+        self.tune_info = sm.last_tune
+        if diagnostics:
+            for k, a in sm.last_tune["accepts"].items():
+                print(f"tune {k}: acceptance per level (rows = step scale "
+                      f"{sm.last_tune['scales'].tolist()}):\n{a / n_burn}")
         if update_vals:
-            sm.write_back(st)
-        self._chain = None
+            sm.write_back()
 
     def do_mcmc(self, nsamp, prog=False, do_propMH=True, no_init=False):
         """SEPIA do_mcmc (src/model.py:235): ``nsamp`` component-wise Metropolis sweeps on the
         GPU, appended to ``samples`` (betaU (N, (d+1) P), lamUz/lamWs (N, P), lamWOs (N, 1),
         logPost (N, 1)); the last state becomes the current parameter values."""
         sm = self._sampler()
-        st, new = sm.run(int(nsamp), self.rng)
-        sm.write_back(st)
+        new = sm.run(int(nsamp), self.rng)
+        sm.write_back()
         if self.samples is None:
             self.samples = new
         else:

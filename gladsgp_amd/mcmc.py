@@ -51,15 +51,20 @@ accepted on the sum.  The whole sweep is stream-ordered device work: no host syn
 proposals and accept/reject are device tensor ops on uniforms drawn on the host from a seeded
 numpy Generator (so a CPU restatement fed the same uniforms reproduces the chain).
 
-tune_step_sizes(n_burn, n_levels): for each level l the steps are default * 2^e_l, e_l evenly
-spaced in [-(n_levels-1)/2, (n_levels-1)/2]; n_burn sweeps are run at each level continuing the
-chain, acceptances are counted per element, and a binomial logistic regression of acceptance on
-log(step) gives the step whose predicted acceptance is 1/e (logit = log(1/(e-1))).  Ladder base,
-target and the pseudo-count regularisation are *unpinned* (GPMSA's stepsize procedure).
+tune_step_sizes(n_burn, n_levels): after n_burn burn-in sweeps at the default steps, for each
+level l the steps are default * 2^e_l, e_l evenly spaced in [-(n_levels-1)/2, (n_levels-1)/2];
+n_burn sweeps are run at each level continuing the chain, acceptances are counted per element, and a binomial logistic regression of acceptance on
+log(step) gives the step whose predicted acceptance is 1/e (logit = log(1/(e-1))), anchored by
+one pseudo-acceptance far below and one pseudo-rejection far above the ladder so that a
+parameter accepted (or rejected) at every level still gets an extrapolated step; the result
+is clamped to the anchors' span, to 1 for BetaRho moves (rho lives in (0, 1]) and to the bound
+width for a bounded parameter.  Burn-in, ladder base, target, regularisation and clamps are
+*unpinned* (GPMSA's stepsize procedure).
 """
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -160,12 +165,14 @@ def propose(p: SepiaParam, x: torch.Tensor, step: torch.Tensor, u: torch.Tensor)
 # --------------------------------------------------------------------------- device sampler
 @dataclass
 class ChainState:
+    """Device-resident chain state; updated in place so a captured sweep graph stays valid."""
+
     betaU: torch.Tensor        # (d+1, P)
     lamUz: torch.Tensor        # (P,)
     lamWs: torch.Tensor        # (P,)
     lamWOs: torch.Tensor       # (1,)
     ll: torch.Tensor           # (P,) current per-GP log-likelihood
-    acc: dict = field(default_factory=dict)   # per-parameter acceptance counters (device)
+    acc: dict = field(default_factory=dict)   # per-element acceptance counters (device)
 
 
 def uniforms_per_sweep(d: int, P: int) -> int:
@@ -174,10 +181,18 @@ def uniforms_per_sweep(d: int, P: int) -> int:
 
 
 class GPUSampler:
-    """Component-wise Metropolis over the P PC-GPs of one emulator, all state on the device."""
+    """Component-wise Metropolis over the P PC-GPs of one emulator, all state on the device.
+
+    One sweep is ~11 batched gp_loglik calls plus elementwise proposal / accept work: a few
+    hundred small launches.  With ``use_graph`` (or GPFIT_MCMC_GRAPH=1) the sweep is captured
+    once as a HIP graph (torch.cuda.CUDAGraph) over static buffers -- chain state, uniforms,
+    step sizes, counters -- and replayed.  Measured at n=512, P=8 the sweep is GPU-bound (11
+    small potrf critical paths) and graph replay was slower (6.9 vs 5.5 ms per sweep), so the
+    default is eager stream-ordered launches; both paths run the same in-place sweep.
+    """
 
     def __init__(self, X: torch.Tensor, w_hat: torch.Tensor, LamSim: torch.Tensor,
-                 params: ModelParams):
+                 params: ModelParams, use_graph: bool | None = None):
         self.X = X.contiguous()
         self.w = w_hat.contiguous()                 # (P, n)
         self.P, self.n = self.w.shape
@@ -190,18 +205,59 @@ class GPUSampler:
         self._s = torch.empty(self.P, dtype=F64, device=self.dev)
         self._delta = torch.empty(self.P, dtype=F64, device=self.dev)
         self._ll = torch.empty(self.P, dtype=F64, device=self.dev)
+        self.nu = uniforms_per_sweep(self.d, self.P)
+        self.u = torch.zeros(self.nu, dtype=F64, device=self.dev)        # static uniforms
+        self.steps = {k: self._t(getattr(params, k).mcmcStepParam) for k in ModelParams.names}
+        self.lp = torch.zeros(1, dtype=F64, device=self.dev)            # log posterior
+        if use_graph is None:
+            use_graph = os.environ.get("GPFIT_MCMC_GRAPH", "0") == "1"
+        self.use_graph = use_graph and self.dev.type == "cuda"
+        self.graph = None
+        self.st = None
 
     def _t(self, a) -> torch.Tensor:
         return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=self.dev)
 
-    def state_from_params(self) -> ChainState:
+    # -- state ---------------------------------------------------------------------------
+    def init_state(self) -> ChainState:
+        """Chain state from params' current values (allocated once; later calls copy)."""
         pr = self.params
-        st = ChainState(self._t(pr.betaU.val), self._t(pr.lamUz.val).reshape(self.P),
-                        self._t(pr.lamWs.val).reshape(self.P), self._t(pr.lamWOs.val).reshape(1),
-                        torch.empty(self.P, dtype=F64, device=self.dev))
-        st.ll = self.loglik(st.betaU, st.lamUz, st.lamWs, st.lamWOs).clone()
-        return st
+        vals = (self._t(pr.betaU.val), self._t(pr.lamUz.val).reshape(self.P),
+                self._t(pr.lamWs.val).reshape(self.P), self._t(pr.lamWOs.val).reshape(1))
+        if self.st is None:
+            z = torch.zeros(self.P, dtype=F64, device=self.dev)
+            self.st = ChainState(*[v.clone() for v in vals], z.clone())
+            self.st.acc = {("betaU", k): z.clone() for k in range(self.d + 1)}
+            self.st.acc.update({"lamUz": z.clone(), "lamWs": z.clone(),
+                                "lamWOs": torch.zeros(1, dtype=F64, device=self.dev)})
+        else:
+            for t, v in zip((self.st.betaU, self.st.lamUz, self.st.lamWs, self.st.lamWOs),
+                            vals):
+                t.copy_(v)
+        self.st.ll.copy_(self.loglik(self.st.betaU, self.st.lamUz, self.st.lamWs,
+                                     self.st.lamWOs))
+        self.reset_counts()
+        return self.st
 
+    def reset_counts(self) -> None:
+        for c in self.st.acc.values():
+            c.zero_()
+
+    def counts(self) -> dict:
+        return {k: v.cpu().numpy() for k, v in self.st.acc.items()}
+
+    def set_steps(self, scale: float = 1.0) -> None:
+        for k in ModelParams.names:
+            self.steps[k].copy_(self._t(getattr(self.params, k).mcmcStepParam * scale))
+
+    def write_back(self) -> None:
+        pr, st = self.params, self.st
+        pr.betaU.val = st.betaU.cpu().numpy().reshape(pr.betaU.val_shape)
+        pr.lamUz.val = st.lamUz.cpu().numpy().reshape(pr.lamUz.val_shape)
+        pr.lamWs.val = st.lamWs.cpu().numpy().reshape(pr.lamWs.val_shape)
+        pr.lamWOs.val = st.lamWOs.cpu().numpy().reshape(pr.lamWOs.val_shape)
+
+    # -- likelihood / posterior ----------------------------------------------------------
     def loglik(self, betaU, lamUz, lamWs, lamWOs) -> torch.Tensor:
         """Per-GP log-likelihood (P,) for the given parameters (one gp_loglik call)."""
         self._beta.copy_(betaU[1:].transpose(0, 1))
@@ -210,16 +266,18 @@ class GPUSampler:
         return kernels.loglik(self.X, self._beta, self._s, self._delta, self.w, self.ws,
                               out=self._ll)
 
-    def log_post(self, st: ChainState) -> torch.Tensor:
-        pr = self.params
+    def log_post(self) -> torch.Tensor:
+        pr, st = self.params, self.st
         lp = st.ll.sum()
         lp = lp + log_prior(pr.betaU, st.betaU).sum() + log_prior(pr.lamUz, st.lamUz).sum()
         lp = lp + log_prior(pr.lamWs, st.lamWs).sum() + log_prior(pr.lamWOs, st.lamWOs).sum()
         return lp
 
-    def sweep(self, st: ChainState, u: torch.Tensor, steps: dict) -> None:
-        """One component-wise Metropolis sweep; ``u`` holds uniforms_per_sweep uniforms."""
-        pr, P, d = self.params, self.P, self.d
+    # -- one sweep -----------------------------------------------------------------------
+    def _sweep(self) -> None:
+        """One component-wise Metropolis sweep on the static buffers (graph-capturable: no
+        allocation that outlives it, no host synchronisation, in-place state updates)."""
+        pr, st, P, d, u, steps = self.params, self.st, self.P, self.d, self.u, self.steps
         o = 0
 
         def take(k):
@@ -227,13 +285,6 @@ class GPUSampler:
             r = u[o:o + k]
             o += k
             return r
-
-        def count(name, acc):
-            c = st.acc.get(name)
-            if c is None:
-                st.acc[name] = acc.to(F64)
-            else:
-                c.add_(acc.to(F64))
 
         # betaU, one row (all P GPs) at a time
         for k in range(d + 1):
@@ -243,15 +294,14 @@ class GPUSampler:
             dlp = log_prior(pr.betaU, cand) - log_prior(pr.betaU, cur)
             if k == 0:                       # dummy x: the likelihood does not depend on it
                 acc = ok & (torch.log(ua) < dlp)
-                st.betaU[0] = torch.where(acc, cand, cur)
             else:
                 trial = st.betaU.clone()
                 trial[k] = cand
                 ll_new = self.loglik(trial, st.lamUz, st.lamWs, st.lamWOs)
                 acc = ok & (torch.log(ua) < ll_new - st.ll + dlp)
-                st.betaU[k] = torch.where(acc, cand, cur)
-                st.ll = torch.where(acc, ll_new, st.ll)
-            count(("betaU", k), acc)
+                st.ll.copy_(torch.where(acc, ll_new, st.ll))
+            st.betaU[k].copy_(torch.where(acc, cand, cur))
+            st.acc[("betaU", k)].add_(acc.to(F64))
         # lamUz, lamWs: all P GPs at once
         for name in ("lamUz", "lamWs"):
             up, ua = take(P), take(P)
@@ -262,9 +312,9 @@ class GPUSampler:
             args[name] = cand
             ll_new = self.loglik(st.betaU, args["lamUz"], args["lamWs"], st.lamWOs)
             acc = ok & (torch.log(ua) < ll_new - st.ll + log_prior(p, cand) - log_prior(p, cur))
-            setattr(st, name, torch.where(acc, cand, cur))
-            st.ll = torch.where(acc, ll_new, st.ll)
-            count(name, acc)
+            cur.copy_(torch.where(acc, cand, cur))
+            st.ll.copy_(torch.where(acc, ll_new, st.ll))
+            st.acc[name].add_(acc.to(F64))
         # lamWOs: shared by every GP, accepted on the sum
         up, ua = take(1), take(1)
         p = pr.lamWOs
@@ -273,31 +323,34 @@ class GPUSampler:
         ll_new = self.loglik(st.betaU, st.lamUz, st.lamWs, cand)
         dl = (ll_new - st.ll).sum() + (log_prior(p, cand) - log_prior(p, cur)).sum()
         acc = ok & (torch.log(ua) < dl)
-        st.lamWOs = torch.where(acc, cand, cur)
-        st.ll = torch.where(acc, ll_new, st.ll)
-        count("lamWOs", acc)
+        cur.copy_(torch.where(acc, cand, cur))
+        st.ll.copy_(torch.where(acc, ll_new, st.ll))
+        st.acc["lamWOs"].add_(acc.to(F64))
+        self.lp.copy_(self.log_post().reshape(1))
 
-    def steps_tensor(self, scale: float = 1.0) -> dict:
-        pr = self.params
-        return {"betaU": self._t(pr.betaU.mcmcStepParam * scale),
-                "lamUz": self._t(pr.lamUz.mcmcStepParam * scale),
-                "lamWs": self._t(pr.lamWs.mcmcStepParam * scale),
-                "lamWOs": self._t(pr.lamWOs.mcmcStepParam * scale)}
+    def _capture(self) -> None:
+        """Record one sweep as a graph (capture does not execute it: the chain is untouched)."""
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._sweep()
+        self.graph = g
 
-    def write_back(self, st: ChainState) -> None:
-        pr = self.params
-        pr.betaU.val = st.betaU.cpu().numpy().reshape(pr.betaU.val_shape)
-        pr.lamUz.val = st.lamUz.cpu().numpy().reshape(pr.lamUz.val_shape)
-        pr.lamWs.val = st.lamWs.cpu().numpy().reshape(pr.lamWs.val_shape)
-        pr.lamWOs.val = st.lamWOs.cpu().numpy().reshape(pr.lamWOs.val_shape)
+    def sweep(self) -> None:
+        if self.use_graph:
+            if self.graph is None:
+                self._capture()
+            self.graph.replay()
+        else:
+            self._sweep()
 
-    def run(self, nsamp: int, rng: np.random.Generator, steps: dict | None = None,
-            st: ChainState | None = None, record: bool = True, block: int = 64):
-        """``nsamp`` sweeps; returns (state, samples dict of numpy arrays or None)."""
-        st = self.state_from_params() if st is None else st
-        steps = self.steps_tensor() if steps is None else steps
-        nu = uniforms_per_sweep(self.d, self.P)
-        P, d = self.P, self.d
+    # -- chains --------------------------------------------------------------------------
+    def run(self, nsamp: int, rng: np.random.Generator, record: bool = True, block: int = 64):
+        """``nsamp`` sweeps from the current state (init_state() first if there is none);
+        returns the samples dict (numpy) when ``record``."""
+        if self.st is None:
+            self.init_state()
+        st, P, d = self.st, self.P, self.d
         if record:
             rec = {"betaU": torch.empty((nsamp, (d + 1) * P), dtype=F64, device=self.dev),
                    "lamUz": torch.empty((nsamp, P), dtype=F64, device=self.dev),
@@ -306,31 +359,36 @@ class GPUSampler:
                    "logPost": torch.empty((nsamp, 1), dtype=F64, device=self.dev)}
         for a in range(0, nsamp, block):
             b = min(nsamp, a + block)
-            U = self._t(rng.random((b - a, nu)))
+            U = self._t(rng.random((b - a, self.nu)))
             for i in range(a, b):
-                self.sweep(st, U[i - a], steps)
+                self.u.copy_(U[i - a])
+                self.sweep()
                 if record:
-                    rec["betaU"][i] = st.betaU.reshape(-1)
-                    rec["lamUz"][i] = st.lamUz
-                    rec["lamWs"][i] = st.lamWs
-                    rec["lamWOs"][i] = st.lamWOs
-                    rec["logPost"][i] = self.log_post(st)
-        samples = {k: v.cpu().numpy() for k, v in rec.items()} if record else None
-        return st, samples
+                    rec["betaU"][i].copy_(st.betaU.reshape(-1))
+                    rec["lamUz"][i].copy_(st.lamUz)
+                    rec["lamWs"][i].copy_(st.lamWs)
+                    rec["lamWOs"][i].copy_(st.lamWOs)
+                    rec["logPost"][i].copy_(self.lp)
+        return {k: v.cpu().numpy() for k, v in rec.items()} if record else None
 
 
 # --------------------------------------------------------------------------- step tuning
 def logistic_step(log_steps: np.ndarray, accepts: np.ndarray, trials: int,
-                  target_logit: float = TARGET_LOGIT, pseudo: float = 0.5) -> float:
-    """Step whose fitted acceptance probability hits the target (binomial logit regression of
-    acceptance on log step, IRLS; ``pseudo`` successes/failures per level keep the fit finite
-    when a level accepts everything or nothing).  Returns exp(log step*)."""
-    x = np.asarray(log_steps, dtype=np.float64)
-    yk = np.asarray(accepts, dtype=np.float64) + pseudo
-    nk = float(trials) + 2.0 * pseudo
+                  target_logit: float = TARGET_LOGIT, pseudo: float = 0.5,
+                  anchor: float = math.log(100.0)) -> float:
+    """Step whose fitted acceptance probability hits the target: binomial logit regression of
+    acceptance on log step (IRLS).  ``pseudo`` successes/failures per level keep the fit
+    finite when a level accepts everything or nothing, and two anchor observations (one
+    acceptance at ``anchor`` below the smallest step, one rejection ``anchor`` above the
+    largest) give the fit a slope when every level accepts (or rejects) almost always, so it
+    extrapolates instead of stalling at the ladder's end.  Returns exp(log step*)."""
+    xl = np.asarray(log_steps, dtype=np.float64)
+    x = np.concatenate([xl, [xl.min() - anchor, xl.max() + anchor]])
+    yk = np.concatenate([np.asarray(accepts, dtype=np.float64) + pseudo, [1.0, 0.0]])
+    nk = np.concatenate([np.full(len(xl), float(trials) + 2.0 * pseudo), [1.0, 1.0]])
     A = np.stack([np.ones_like(x), x], axis=1)
     bvec = np.zeros(2)
-    for _ in range(50):
+    for _ in range(100):
         eta = A @ bvec
         p = 1.0 / (1.0 + np.exp(-eta))
         wgt = nk * p * (1.0 - p)
@@ -344,42 +402,65 @@ def logistic_step(log_steps: np.ndarray, accepts: np.ndarray, trials: int,
         if np.max(np.abs(dlt)) < 1e-10:
             break
     b0, b1 = bvec
-    rate = yk / nk
-    if not np.isfinite(b1) or b1 >= -1e-12:
-        # acceptance should fall as the step grows; otherwise take the closest level
-        return float(np.exp(x[int(np.argmin(np.abs(rate - 1.0 / math.e)))]))
+    if not np.all(np.isfinite(bvec)) or b1 >= -1e-12:
+        rate = (yk / nk)[: len(xl)]
+        return float(np.exp(xl[int(np.argmin(np.abs(rate - 1.0 / math.e)))]))
     return float(np.exp((target_logit - b0) / b1))
 
 
 def tune_step_sizes(sampler: GPUSampler, n_burn: int, n_levels: int,
-                    rng: np.random.Generator, st: ChainState | None = None) -> ChainState:
+                    rng: np.random.Generator) -> None:
     """GPMSA-style step-size tuning (see module doc); updates params' mcmcStepParam in place
-    and returns the chain state reached."""
+    and leaves the sampler's chain at the state reached."""
     pr = sampler.params
-    st = sampler.state_from_params() if st is None else st
+    if sampler.st is None:
+        sampler.init_state()
     ex = np.linspace(-(n_levels - 1) / 2.0, (n_levels - 1) / 2.0, n_levels)
     base = {k: getattr(pr, k).mcmcStepParam.copy() for k in ModelParams.names}
+    # burn-in at the default steps first: acceptance counted while the chain is still
+    # travelling from the start values would make the smallest-step level look worst
+    sampler.set_steps(1.0)
+    sampler.run(n_burn, rng, record=False)
     counts = []
     for e in ex:
-        scale = 2.0 ** e
-        st.acc = {}
-        st, _ = sampler.run(n_burn, rng, steps=sampler.steps_tensor(scale), st=st, record=False)
-        counts.append({k: v.cpu().numpy() for k, v in st.acc.items()})
+        sampler.set_steps(2.0 ** e)
+        sampler.reset_counts()
+        sampler.run(n_burn, rng, record=False)
+        counts.append(sampler.counts())
     logs = {k: np.log(base[k][None] * (2.0 ** ex).reshape((-1,) + (1,) * base[k].ndim))
             for k in base}
     P, d = sampler.P, sampler.d
     new = {k: base[k].copy() for k in base}
+
+    def fit(name, x, acc):
+        # clamp: the anchors' span, rho's range for BetaRho moves, the bound width
+        p = getattr(pr, name)
+        st_ = logistic_step(x, acc, n_burn)
+        lo_c, hi_c = math.exp(x.min() - math.log(100.0)), math.exp(x.max() + math.log(100.0))
+        if p.mcmcStepType == "BetaRho":
+            hi_c = min(hi_c, 1.0)
+        elif np.isfinite(p.bounds[0]) and np.isfinite(p.bounds[1]):
+            hi_c = min(hi_c, p.bounds[1] - p.bounds[0])
+        return float(np.clip(st_, lo_c, max(hi_c, lo_c)))
+
     for k in range(d + 1):
         for j in range(P):
             acc = np.array([c[("betaU", k)][j] for c in counts])
-            new["betaU"][k, j] = logistic_step(logs["betaU"][:, k, j], acc, n_burn)
+            new["betaU"][k, j] = fit("betaU", logs["betaU"][:, k, j], acc)
     for name in ("lamUz", "lamWs"):
         for j in range(P):
             acc = np.array([c[name][j] for c in counts])
-            new[name][0, j] = logistic_step(logs[name][:, 0, j], acc, n_burn)
+            new[name][0, j] = fit(name, logs[name][:, 0, j], acc)
     acc = np.array([c["lamWOs"][0] for c in counts])
-    new["lamWOs"][0, 0] = logistic_step(logs["lamWOs"][:, 0, 0], acc, n_burn)
+    new["lamWOs"][0, 0] = fit("lamWOs", logs["lamWOs"][:, 0, 0], acc)
     for k in base:
         getattr(pr, k).mcmcStepParam = new[k]
-    st.acc = {}
-    return st
+    sampler.set_steps(1.0)
+    sampler.reset_counts()
+    sampler.last_tune = {"scales": 2.0 ** ex, "trials": n_burn, "base": base, "new": new,
+                         "accepts": {
+                             "betaU": np.array([[c[("betaU", k)] for k in range(d + 1)]
+                                                for c in counts]),
+                             "lamUz": np.array([c["lamUz"] for c in counts]),
+                             "lamWs": np.array([c["lamWs"] for c in counts]),
+                             "lamWOs": np.array([c["lamWOs"] for c in counts])}}

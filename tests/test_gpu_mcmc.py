@@ -71,15 +71,17 @@ def _spec(pr):
                 getattr(pr, k).mcmcStepType) for k in pr.names}
 
 
-@pytest.mark.parametrize("n,d,P,steps_scale", [(48, 2, 3, 1.0), (130, 3, 2, 0.3)])
-def test_chain_matches_oracle(dev, n, d, P, steps_scale):
+@pytest.mark.parametrize("n,d,P,steps_scale,graph", [(48, 2, 3, 1.0, False),
+                                                     (48, 2, 3, 1.0, True),
+                                                     (130, 3, 2, 0.3, True)])
+def test_chain_matches_oracle(dev, n, d, P, steps_scale, graph):
     X, w, lam = _problem(n, d, P, seed=11 + n)
     pr = mcmc.ModelParams(d, P)
     for k in pr.names:
         getattr(pr, k).mcmcStepParam = getattr(pr, k).mcmcStepParam * steps_scale
-    sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr)
+    sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr, use_graph=graph)
     nsw = 25
-    st, rec = sampler.run(nsw, np.random.default_rng(5))
+    rec = sampler.run(nsw, np.random.default_rng(5))
     U = np.random.default_rng(5).random((nsw, mcmc.uniforms_per_sweep(d, P)))
     state = {"betaU": pr.betaU.val, "lamUz": pr.lamUz.val[0], "lamWs": pr.lamWs.val[0],
              "lamWOs": pr.lamWOs.val[0, 0]}
@@ -97,11 +99,12 @@ def test_tune_and_sample(dev):
     pr = mcmc.ModelParams(d, P)
     sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr)
     rng = np.random.default_rng(0)
-    st = mcmc.tune_step_sizes(sampler, 20, 3, rng)
+    mcmc.tune_step_sizes(sampler, 20, 3, rng)
     for k in pr.names:
         stp = getattr(pr, k).mcmcStepParam
         assert np.all(np.isfinite(stp)) and np.all(stp > 0), k
-    st, rec = sampler.run(40, rng, st=st)
+    assert sampler.last_tune["accepts"]["lamUz"].shape == (3, P)
+    rec = sampler.run(40, rng)
     assert rec["betaU"].shape == (40, (d + 1) * P)
     assert np.all(np.isfinite(rec["logPost"]))
 

@@ -19,16 +19,19 @@ def test_logistic_step_recovers_target():
     acc = np.round(p * trials)
     got = mcmc.logistic_step(np.log(steps), acc, trials, pseudo=0.0)
     want = math.exp((mcmc.TARGET_LOGIT - b0) / b1)
-    assert abs(got / want - 1) < 1e-3
+    assert abs(got / want - 1) < 1e-3     # the two unit-weight anchors barely move a 1e5 fit
 
 
 def test_logistic_step_degenerate_levels():
     steps = np.log(np.array([0.1, 0.2, 0.4]))
-    # everything accepted at every level: no slope -> closest level to 1/e (largest step)
-    got = mcmc.logistic_step(steps, np.array([20, 20, 20]), 20)
-    assert got > 0 and np.isfinite(got)
-    # acceptance rising with the step (wrong sign) -> a ladder value
-    got = mcmc.logistic_step(steps, np.array([1, 5, 15]), 20)
+    # everything accepted at every level: the anchors extrapolate beyond the ladder
+    got = mcmc.logistic_step(steps, np.array([100, 100, 100]), 100)
+    assert np.isfinite(got) and got > 0.4
+    # nothing accepted: extrapolate below it
+    got = mcmc.logistic_step(steps, np.array([0, 0, 0]), 100)
+    assert np.isfinite(got) and got < 0.1
+    # acceptance rising steeply with the step (wrong sign) -> a ladder value
+    got = mcmc.logistic_step(steps, np.array([0, 50, 100]), 100)
     assert np.isclose(np.log(got), steps).any()
 
 
