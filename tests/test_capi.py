@@ -30,7 +30,8 @@ def lib():
 def test_header_declares_expected_entry_points():
     names = _declared()
     for must in ("gp_gram_ardse", "gp_cross_ardse", "gp_potrf_inv", "gp_predict",
-                 "gp_predict_ws_bytes", "gp_nll", "gp_trmv", "gp_padded_n", "gp_version"):
+                 "gp_predict_ws_bytes", "gp_nll", "gp_trmv", "gp_padded_n", "gp_version",
+                 "gp_loglik", "gp_loglik_ws_bytes"):
         assert must in names
 
 
@@ -80,6 +81,17 @@ def test_argument_validation_returns_lapack_style_codes(lib):
     assert rc == -22  # workspace too small
     # zero-sized problems are a no-op
     assert lib.gp_potrf_inv(dummy, 0, 1, 0, dummy, 1, 0, 1, None, None, None) == 0
+    # gp_loglik: workspace size grows with the batch; bad args rejected before any launch
+    assert lib.gp_loglik_ws_bytes(512, 8) > lib.gp_loglik_ws_bytes(512, 1) > 512 * 512 * 8
+    assert lib.gp_loglik_ws_bytes(-1, 1) == -1
+    rc = lib.gp_loglik(dummy, 64, 0, 2, dummy, 2, dummy, dummy, dummy, 64, 1, dummy, 1 << 30,
+                       dummy, None, None)
+    assert rc == -3   # d < 1
+    rc = lib.gp_loglik(dummy, 64, 2, 2, dummy, 2, dummy, dummy, dummy, 64, 2, dummy, 16,
+                       dummy, None, None)
+    assert rc == -13  # workspace too small
+    assert lib.gp_loglik(dummy, 0, 2, 2, dummy, 2, dummy, dummy, dummy, 0, 1, None, 0, dummy,
+                         None, None) == 0
 
 
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
