@@ -133,7 +133,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workload", choices=("c3", "c4"), default="c3")
     ap.add_argument("--serial", action="store_true",
-                    help="c3: no side-stream overlap of cross-covariance and factorisation")
+                    help="c3: one stream, no overlap at all (gram, potrf, predict in order)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="c3: alternate two streams so the next step's factorisation runs "
+                         "under the current TRMM (measured no gain: the TRMM holds every CU "
+                         "slot and the factorisation's launches wait behind it)")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
     args = ap.parse_args()
     if args.workload == "c4":
@@ -149,20 +153,31 @@ def main():
     bd = torch.as_tensor(beta, device=dev).reshape(1, d)
     sd = torch.tensor([s], dtype=torch.float64, device=dev)
     dd = torch.tensor([delta], dtype=torch.float64, device=dev)
-    ws = kernels.PredictWorkspace()
-    mean = torch.empty((1, m), dtype=torch.float64, device=dev)
-    var = torch.empty((1, m), dtype=torch.float64, device=dev)
+    # Default: one gp_fit_predict per step on the current stream (its cross-covariance runs
+    # on a library stream while the factorisation runs).  --pipeline alternates two streams
+    # and two buffer sets so step t+1's Gram + factorisation + cross-covariance run under step
+    # t's TRMM; every step still does all of its own work inside the timed region.
+    nslot = 2 if (args.pipeline and not args.serial) else 1
+    streams = ([torch.cuda.current_stream(dev)] if nslot == 1 else
+               [torch.cuda.Stream(device=dev) for _ in range(nslot)])
+    wss = [kernels.PredictWorkspace() for _ in range(nslot)]
+    outs = [(torch.empty((1, m), dtype=torch.float64, device=dev),
+             torch.empty((1, m), dtype=torch.float64, device=dev)) for _ in range(nslot)]
+    mean, var = outs[0]
+    counter = [0]
 
     def step():
+        sl = counter[0] % nslot
+        counter[0] += 1
         if args.serial:
             G = kernels.gram(Xd, bd, sd, dd)
             ch = kernels.cholesky_inverse(G)
-            kernels.predict(ch, Xd, Xsd, bd, sd, sd, yd, m_chunk=args.m_chunk, workspace=ws,
-                            out=(mean, var))
+            kernels.predict(ch, Xd, Xsd, bd, sd, sd, yd, m_chunk=args.m_chunk,
+                            workspace=wss[sl], out=outs[sl])
             return ch
-        # cross-covariance on a side stream while the factorisation runs (within one step)
-        _, _, ch = kernels.fit_predict(Xd, Xsd, bd, sd, dd, sd, yd, m_chunk=args.m_chunk,
-                                       workspace=ws, out=(mean, var))
+        with torch.cuda.stream(streams[sl]):
+            _, _, ch = kernels.fit_predict(Xd, Xsd, bd, sd, dd, sd, yd, m_chunk=args.m_chunk,
+                                           workspace=wss[sl], out=outs[sl])
         return ch
 
     for _ in range(args.warmup):
@@ -238,7 +253,12 @@ def main():
         "data": "synthetic (SURVEY §8d C3 recipe: seeded uniform design, sin target)",
         "config": {"workload": "C3 single-output ARD-SE GP: Gram + Cholesky/L^-1 + predict",
                    "n_train": n, "m_test_per_gpu": m, "d": d,
-                   "parallelism": f"test-point shards x{ctx.world}, redundant factorisation"},
+                   "parallelism": f"test-point shards x{ctx.world}, redundant factorisation",
+                   "pipeline": ("serial" if args.serial else
+                                "gp_fit_predict (cross-covariance overlapped with the "
+                                "factorisation)" if nslot == 1 else
+                                "gp_fit_predict, 2 alternating streams (next factorisation "
+                                "under the current TRMM)")},
         "roofline": roof, "roofline_aux": aux, "cpu_baseline": None,
     }
     if ctx.world == 1 and not args.no_cpu:

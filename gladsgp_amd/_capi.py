@@ -46,6 +46,12 @@ SIGNATURES = {
                         c_void_p]),
     "gp_nll": (c_int, [c_void_p, c_int, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p,
                        c_void_p, c_int, c_void_p]),
+    "gp_fit_predict_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
+    "gp_fit_predict": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                               c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                               c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int,
+                               c_void_p]),
     "gp_loglik_ws_bytes": (c_ll, [c_int, c_int]),
     "gp_loglik": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                           c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,

@@ -4,25 +4,27 @@
 //             (examples/02...ipynb:70-72, no 2pi term) and the per-PC quadratic form + logdet
 //             of SEPIA's logLik (src/model.py:234-235 drives it through do_mcmc).
 #include "gpfit_common.h"
+#include "gpfit_internal.h"
 #include "../../include/gpfit.h"
 
 namespace {
 
-// z_b[r] = sum_{k<=r, k<n} Linv_b[r,k] w_b[k] for r < rows.  1024 threads = 64 rows x 16
+// z_b[r] = sum_{k<=r, k<n} Linv_b[r,k] w_b[k] for r0 <= r < rows.  1024 threads = 64 rows x 16
 // k-slices: each wave reads 64 consecutive rows of one column (512 B, coalesced), the 16
 // partial sums meet in LDS.  Reads the n^2/2 lower triangle once: HBM-bound.
 constexpr int kTrmvSlices = 16;
 __global__ __launch_bounds__(1024) void trmv_kernel(const double* __restrict__ Linv, int ld,
                                                     long long sL, const double* __restrict__ w,
                                                     int ldw, double* __restrict__ z, int ldz,
-                                                    int rows, int n) {
+                                                    int r0, int rows, int n) {
   const int b = blockIdx.y;
-  const int r = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rb = r0 + blockIdx.x * 64;
+  const int r = rb + (threadIdx.x & 63);
   const int ks = threadIdx.x >> 6;
   const double* L = Linv + b * sL;
   const double* wb = w + (long long)b * ldw;
   double acc0 = 0.0, acc1 = 0.0;
-  const int kend = min(blockIdx.x * 64 + 64, n);   // block-uniform bound; L is zero above r
+  const int kend = min(rb + 64, n);   // block-uniform bound; L is zero above r
   if (r < rows) {
     int k = ks;
     for (; k + kTrmvSlices < kend; k += 2 * kTrmvSlices) {
@@ -68,12 +70,19 @@ __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restric
 
 }  // namespace
 
+hipError_t gpfit_trmv_rows_launch(const double* Linv, int ld, long long sL, const double* w,
+                                  int ldw, double* z, int ldz, int r0, int r1, int n, int batch,
+                                  hipStream_t st) {
+  if (r1 <= r0 || batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(trmv_kernel, dim3(gp_ceil_div(r1 - r0, 64), batch), dim3(1024), 0, st,
+                     Linv, ld, sL, w, ldw, z, ldz, r0, r1, n);
+  return hipGetLastError();
+}
+
 hipError_t gpfit_trmv_launch(const double* Linv, int ld, long long sL, const double* w,
                              int ldw, double* z, int ldz, int rows, int n, int batch,
                              hipStream_t st) {
-  hipLaunchKernelGGL(trmv_kernel, dim3(gp_ceil_div(rows, 64), batch), dim3(1024), 0, st, Linv,
-                     ld, sL, w, ldw, z, ldz, rows, n);
-  return hipGetLastError();
+  return gpfit_trmv_rows_launch(Linv, ld, sL, w, ldw, z, ldz, 0, rows, n, batch, st);
 }
 
 extern "C" int gp_trmv(const double* Linv, int ldinv, long long strideInv, int n,

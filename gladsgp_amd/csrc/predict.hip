@@ -19,17 +19,16 @@
 #include "gpfit_common.h"
 #include <cstdlib>
 #include "gpfit_profile.h"
+#include "gpfit_internal.h"
 #include "../../include/gpfit.h"
+#include <mutex>
+#include <vector>
 
 hipError_t gpfit_ardse_launch(const double* XA, int na, int ldxa, const double* XB, int nb,
                               int ldxb, int d, const double* beta, int ldbeta,
                               const double* s, const double* delta, double* out, int ldo,
                               long long stride_o, int rows_out, int cols_out, int batch,
                               hipStream_t st);
-hipError_t gpfit_trmv_launch(const double* Linv, int ld, long long sL, const double* w,
-                             int ldw, double* z, int ldz, int rows, int n, int batch,
-                             hipStream_t st);
-
 namespace {
 
 constexpr int BI = 128;   // V tile rows (L^-1 rows)
@@ -298,7 +297,7 @@ Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
   p.slab_elems = (long long)batch * mc * p.npad;
   long long z = (long long)batch * p.npad;
   long long kt = p.slab_elems * p.slabs;
-  long long part = (long long)batch * 2 * p.NI * mc;
+  const long long part = (long long)batch * 2 * p.NI * mc;
   p.off_z = 0;
   p.off_kt = ((z * 8 + 255) / 256) * 256;
   p.off_part = p.off_kt + ((kt * 8 + 255) / 256) * 256;
@@ -314,6 +313,11 @@ extern "C" long long gp_predict_ws_bytes(int n, int m, int batch, int m_chunk) {
 }
 
 extern "C" long long gp_predict_prepared_ws_bytes(int n, int m, int batch, int m_chunk) {
+  if (n <= 0 || m <= 0 || batch <= 0) return 0;
+  return make_plan(n, m, batch, m_chunk, true).bytes;
+}
+
+extern "C" long long gp_fit_predict_ws_bytes(int n, int m, int batch, int m_chunk) {
   if (n <= 0 || m <= 0 || batch <= 0) return 0;
   return make_plan(n, m, batch, m_chunk, true).bytes;
 }
@@ -466,6 +470,101 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
   for (int ch = 0; ch < p.nchunks; ++ch)
     GP_CK(solve_chunk(p, ch, w, w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
                       s_pred, mean, var, ldo, batch, stream));
+#undef GP_CK
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// gp_fit_predict: Gram -> Cholesky/L^-1 -> predict as one stream-ordered operation on `stream`,
+// internally forked over three library streams (equal priority):
+//   fact: Gram, then the blocked factorisation (latency-bound, few CUs busy);
+//   aux : the cross-covariance of every chunk (independent of the factorisation);
+//   pred: once both are done, z = L^-1 w, then per chunk the TRMM (all row tiles of the
+//         chunk, so its K* stays cached) and its mean / var.
+// The operation joins back into `stream`.  A caller that alternates two streams (and two
+// buffer sets) between consecutive calls gets the next problem's factorisation and
+// cross-covariance running under the current problem's TRMM: the fact/aux streams only wait
+// for their own call's inputs, not for the previous call's prediction.
+namespace {
+
+struct FitPredictStreams {
+  hipStream_t fact = nullptr, aux = nullptr, pred = nullptr;
+  hipEvent_t e_start = nullptr, e_fact = nullptr, e_aux = nullptr, e_done = nullptr;
+};
+std::mutex g_fp_mu;
+FitPredictStreams g_fp[64];
+
+hipError_t fit_predict_streams(FitPredictStreams** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(g_fp_mu);
+  FitPredictStreams& S = g_fp[dev];
+  if (!S.fact) {
+    hipStream_t* st[3] = {&S.fact, &S.aux, &S.pred};
+    for (hipStream_t* p : st)
+      if ((e = hipStreamCreateWithFlags(p, hipStreamNonBlocking)) != hipSuccess) return e;
+    hipEvent_t* ev[4] = {&S.e_start, &S.e_fact, &S.e_aux, &S.e_done};
+    for (hipEvent_t* p : ev)
+      if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
+  }
+  *out = &S;
+  return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ldxs, int n,
+                              int m, int d, const double* beta, int ldbeta, const double* s,
+                              const double* delta, const double* s_pred, const double* w_hat,
+                              int ldw, double* G, int ldg, long long strideG, double* Linv,
+                              int ldinv, long long strideInv, int* info, double* logdet,
+                              double* mean, double* var, int ldo, int batch, void* ws,
+                              long long ws_bytes, int m_chunk, hipStream_t stream) {
+  int rc = check_common(X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch);
+  if (rc) return rc;
+  rc = check_solve(Linv, ldinv, strideInv, n, s_pred, w_hat, ldw, m, mean, var, ldo, batch);
+  if (rc) return rc;
+  if (!delta) return -24;
+  if (!G) return -25;
+  if (ldg < n || (batch > 1 && strideG < (long long)ldg * n)) return -26;
+  if (n == 0 || m == 0 || batch == 0) return 0;
+  if (m_chunk < 0) return -23;
+  const Plan p = make_plan(n, m, batch, m_chunk, true);
+  if (!ws) return -21;
+  if (ws_bytes < p.bytes) return -22;
+  const WS w = carve(p, ws);
+  FitPredictStreams* S = nullptr;
+  hipError_t e;
+#define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
+  GP_CK(fit_predict_streams(&S));
+  GP_CK(hipEventRecord(S->e_start, stream));
+  GP_CK(hipStreamWaitEvent(S->fact, S->e_start, 0));
+  GP_CK(hipStreamWaitEvent(S->aux, S->e_start, 0));
+  // aux: cross-covariance of every chunk
+  for (int ch = 0; ch < p.nchunks; ++ch)
+    GP_CK(cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n, m, d,
+                      beta, ldbeta, s, batch, S->aux));
+  GP_CK(hipEventRecord(S->e_aux, S->aux));
+  // fact: Gram -> Cholesky / L^-1
+  rc = gp_gram_ardse(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, S->fact);
+  if (rc) return rc;
+  rc = gp_potrf_inv(G, n, ldg, strideG, Linv, ldinv, strideInv, batch, info, logdet, S->fact);
+  if (rc) return rc;
+  GP_CK(hipEventRecord(S->e_fact, S->fact));
+  // pred: z, then TRMM + mean / var chunk by chunk.  One launch per chunk (not one for all):
+  // the dispatcher interleaves another stream's kernels between launches, so a concurrent
+  // factorisation is not starved behind a 25 ms grid (measured: 14 ms vs 3 ms per potrf).
+  GP_CK(hipStreamWaitEvent(S->pred, S->e_fact, 0));
+  GP_CK(hipStreamWaitEvent(S->pred, S->e_aux, 0));
+  GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
+                          S->pred));
+  for (int ch = 0; ch < p.nchunks; ++ch)
+    GP_CK(solve_chunk(p, ch, w, w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
+                      s_pred, mean, var, ldo, batch, S->pred));
+  GP_CK(hipEventRecord(S->e_done, S->pred));
+  GP_CK(hipStreamWaitEvent(stream, S->e_done, 0));
 #undef GP_CK
   return 0;
 }

@@ -309,9 +309,47 @@ def side_stream(device) -> torch.cuda.Stream:
 
 def fit_predict(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
                 workspace: PredictWorkspace | None = None, out=None):
-    """Gram -> Cholesky/L^-1 -> predict for ``batch`` GPs with the cross-covariance built on a
-    side stream concurrently with the (latency-bound) factorisation.  Returns (mean, var, chol).
-    """
+    """Gram -> Cholesky/L^-1 -> predict for ``batch`` GPs in one gp_fit_predict call: the
+    cross-covariance and the TRMM of every finished 128-row tile of L^-1 run on a low-priority
+    library stream while the factorisation (high priority) continues.  Returns
+    (mean, var, chol)."""
+    dev = X.device
+    X = _as_f64(X, dev, "X")
+    Xs = _as_f64(Xs, dev, "Xs")
+    n, d = X.shape
+    m = Xs.shape[0]
+    bt = torch.as_tensor(beta)
+    batch = bt.shape[0] if bt.dim() == 2 else 1
+    beta_t = _beta(beta, batch, d, dev)
+    s_t = _per_batch(s, batch, dev, "s")
+    d_t = _per_batch(delta, batch, dev, "delta")
+    sp_t = _per_batch(s_pred, batch, dev, "s_pred")
+    w_t = _as_f64(w, dev, "w").reshape(batch, n)
+    npad = padded_n(n)
+    G = torch.empty((batch, n, n), dtype=F64, device=dev)
+    Linv = torch.empty((batch, npad, npad), dtype=F64, device=dev)
+    info = torch.empty(batch, dtype=torch.int32, device=dev)
+    logdet = torch.empty(batch, dtype=F64, device=dev)
+    if out is None:
+        mean = torch.empty((batch, m), dtype=F64, device=dev)
+        var = torch.empty((batch, m), dtype=F64, device=dev)
+    else:
+        mean, var = out
+    nbytes = _capi.lib().gp_fit_predict_ws_bytes(n, m, batch, int(m_chunk))
+    ws = (workspace or PredictWorkspace()).get(nbytes, dev)
+    _capi.call("gp_fit_predict", X.data_ptr(), d, Xs.data_ptr(), d, n, m, d, beta_t.data_ptr(),
+               d, s_t.data_ptr(), d_t.data_ptr(), sp_t.data_ptr(), w_t.data_ptr(), n,
+               G.data_ptr(), n, n * n, Linv.data_ptr(), npad, npad * npad, info.data_ptr(),
+               logdet.data_ptr(), mean.data_ptr(), var.data_ptr(),
+               mean.stride(0) if batch > 1 else m, batch, ws.data_ptr(), ws.numel(),
+               int(m_chunk), _stream(dev))
+    return mean, var, Cholesky(n, G, Linv, info, logdet)
+
+
+def fit_predict_streams(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
+                        workspace: PredictWorkspace | None = None, out=None):
+    """Previous scheme (kept for comparison): cross-covariance on a torch side stream during
+    the factorisation, then the whole TRMM after it.  Returns (mean, var, chol)."""
     dev = X.device
     bt = torch.as_tensor(beta)
     batch = bt.shape[0] if bt.dim() == 2 else 1

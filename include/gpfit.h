@@ -135,6 +135,27 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
            int batch, hipStream_t stream);
 
 /*
+ * Fit + predict in one call:
+ *   G = gram(X) (caller buffer, L on return) -> L, L^-1, info, logdet (as gp_potrf_inv) ->
+ *   mean / var at the m test points (as gp_predict).
+ * Forks from `stream` into three library-owned streams (Gram + factorisation | cross-
+ * covariance of every chunk | then per chunk the TRMM + mean/var) and joins
+ * back; the caller sees one stream-ordered operation.  Callers that alternate two streams and
+ * two buffer sets between consecutive calls overlap the next factorisation with the current
+ * TRMM.  `ws` holds gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes.  Not re-entrant
+ * across host threads on the same device (the internal streams are shared).
+ * Replaces the reference's fit-then-predict sequence per GP (SEPIA likelihood factorisation +
+ * SepiaEmulatorPrediction, time_predictions.py:76-79) at the bench configuration.
+ */
+long long gp_fit_predict_ws_bytes(int n, int m, int batch, int m_chunk);
+int gp_fit_predict(const double* X, int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                   const double* beta, int ldbeta, const double* s, const double* delta,
+                   const double* s_pred, const double* w_hat, int ldw, double* G, int ldg,
+                   long long strideG, double* Linv, int ldinv, long long strideInv, int* info,
+                   double* logdet, double* mean, double* var, int ldo, int batch, void* ws,
+                   long long ws_bytes, int m_chunk, hipStream_t stream);
+
+/*
  * Batched GP log-likelihood in one stream-ordered call: Gram (gp_gram_ardse) -> Cholesky
  * (gp_potrf_inv) -> ll[b] = -(1/2 ||L_b^-1 w_b||^2 + 1/2 log|G_b|), no 2*pi term, with
  * ll[b] = -inf where the factorisation failed (info[b] != 0, optionally copied out to `info`).

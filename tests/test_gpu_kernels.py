@@ -260,7 +260,14 @@ def test_two_phase_predict_and_overlap_match_single(dev):
     prep = kernels.predict_prepare(Xd, Xsd, _t(betas, dev), _t(s, dev), batch=B, m_chunk=1024)
     m2, v2 = kernels.predict_solve(ch, prep, _t(s, dev), _t(W, dev))
     assert torch.equal(m1, m2) and torch.equal(v1, v2)
-    m3, v3, _ = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
-                                    _t(s, dev), _t(W, dev), m_chunk=1024)
+    # gp_fit_predict: the TRMM of finished L^-1 row tiles overlapped with the factorisation
+    m3, v3, ch3 = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                      _t(s, dev), _t(W, dev), m_chunk=1024)
     torch.cuda.synchronize()
     assert torch.equal(m1, m3) and torch.equal(v1, v3)
+    assert torch.equal(ch3.L, ch.L) and torch.equal(ch3.Linv, ch.Linv)
+    assert torch.equal(ch3.logdet, ch.logdet) and int(ch3.info.abs().sum()) == 0
+    m4, v4, _ = kernels.fit_predict_streams(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                            _t(s, dev), _t(W, dev), m_chunk=1024)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m4) and torch.equal(v1, v4)
