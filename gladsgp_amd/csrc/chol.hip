@@ -19,6 +19,7 @@
 // second wave applying the same row operations to I (L^-1); see the function.
 #include "gpfit_common.h"
 #include "gpfit_profile.h"
+#include "gpfit_internal.h"
 #include "../../include/gpfit.h"
 
 #ifdef GPFIT_DIAG_PROBE
@@ -487,9 +488,18 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(
 
 }  // namespace
 
+static_assert(GPFIT_POTRF_NB == NB, "gpfit_internal.h must match the blocking");
+
 extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double* Linv,
                             int ldinv, long long strideInv, int batch, int* info,
                             double* logdet, hipStream_t stream) {
+  return gpfit_potrf_inv_event(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,
+                               stream, -1, nullptr);
+}
+
+int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
+                          int ldinv, long long strideInv, int batch, int* info, double* logdet,
+                          hipStream_t stream, int k_ev, hipEvent_t ev) {
   if (!A) return -1;
   if (n < 0) return -2;
   if (lda < n || lda < 1) return -3;
@@ -532,6 +542,7 @@ extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double
                          strideA, Linv, ldinv, strideInv, n, k, T, info, logdet);
       GP_CK(hipGetLastError());
     }
+    if (ev && (k == k_ev || (k == N - 1 && k_ev >= N))) GP_CK(hipEventRecord(ev, stream));
   }
   gpfit_prof_end(GP_PROF_POTRF, stream);
 #undef GP_CK

@@ -9,3 +9,12 @@ hipError_t gpfit_trmv_rows_launch(const double* Linv, int ld, long long sL, cons
 hipError_t gpfit_trmv_launch(const double* Linv, int ld, long long sL, const double* w,
                              int ldw, double* z, int ldz, int rows, int n, int batch,
                              hipStream_t st);
+
+constexpr int GPFIT_POTRF_NB = 64;   // column block of gp_potrf_inv (chol.hip NB)
+
+// gp_potrf_inv that also records `ev` on the stream once block step `k_ev` (NB = 64 columns)
+// has been enqueued (k_ev clamped to the last step); chol.hip.  Lets a caller start HBM-bound
+// side work only when the factorisation turns latency-bound.
+int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
+                          int ldinv, long long strideInv, int batch, int* info, double* logdet,
+                          hipStream_t stream, int k_ev, hipEvent_t ev);

@@ -490,7 +490,23 @@ namespace {
 struct FitPredictStreams {
   hipStream_t fact = nullptr, aux = nullptr, pred = nullptr;
   hipEvent_t e_start = nullptr, e_fact = nullptr, e_aux = nullptr, e_done = nullptr;
+  hipEvent_t e_late = nullptr;   // the factorisation has turned latency-bound
 };
+
+// Block step of the n/64 blocked factorisation from which the HBM-bound cross-covariance runs
+// beside it.  Started at once it doubles the early (bandwidth-bound) trailing updates
+// (54 -> 123 us); started in the latency-bound tail it fills idle bandwidth.  Sweep at C3
+// (20 steps): start fraction 0 / 0.5 / 0.6 / 0.7 / 0.8 -> 30.2 / 29.85 / 29.78 / 29.85 /
+// 30.07 ms per step (later than ~0.7 the cross-covariance outlasts the factorisation).
+// GPFIT_CROSS_START (fraction of the steps, 0 = at once) overrides.
+int late_step(int nblk) {
+  static double f = [] {
+    const char* e = getenv("GPFIT_CROSS_START");
+    return e ? atof(e) : 0.6;
+  }();
+  const int k = (int)(f * nblk);
+  return k < 0 ? 0 : k;
+}
 std::mutex g_fp_mu;
 FitPredictStreams g_fp[64];
 
@@ -505,7 +521,7 @@ hipError_t fit_predict_streams(FitPredictStreams** out) {
     hipStream_t* st[3] = {&S.fact, &S.aux, &S.pred};
     for (hipStream_t* p : st)
       if ((e = hipStreamCreateWithFlags(p, hipStreamNonBlocking)) != hipSuccess) return e;
-    hipEvent_t* ev[4] = {&S.e_start, &S.e_fact, &S.e_aux, &S.e_done};
+    hipEvent_t* ev[5] = {&S.e_start, &S.e_fact, &S.e_aux, &S.e_done, &S.e_late};
     for (hipEvent_t* p : ev)
       if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
   }
@@ -541,18 +557,22 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   GP_CK(fit_predict_streams(&S));
   GP_CK(hipEventRecord(S->e_start, stream));
   GP_CK(hipStreamWaitEvent(S->fact, S->e_start, 0));
-  GP_CK(hipStreamWaitEvent(S->aux, S->e_start, 0));
-  // aux: cross-covariance of every chunk
+  // fact: Gram -> Cholesky / L^-1, with e_late once the factorisation is latency-bound
+  rc = gp_gram_ardse(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, S->fact);
+  if (rc) return rc;
+  const int nblk = gp_ceil_div(n, GPFIT_POTRF_NB);
+  const int k_late = late_step(nblk);
+  if (k_late == 0) GP_CK(hipEventRecord(S->e_late, S->fact));
+  rc = gpfit_potrf_inv_event(G, n, ldg, strideG, Linv, ldinv, strideInv, batch, info, logdet,
+                             S->fact, k_late > 0 ? k_late : -1, k_late > 0 ? S->e_late : nullptr);
+  if (rc) return rc;
+  GP_CK(hipEventRecord(S->e_fact, S->fact));
+  // aux: cross-covariance of every chunk, from the factorisation's latency-bound phase on
+  GP_CK(hipStreamWaitEvent(S->aux, S->e_late, 0));
   for (int ch = 0; ch < p.nchunks; ++ch)
     GP_CK(cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n, m, d,
                       beta, ldbeta, s, batch, S->aux));
   GP_CK(hipEventRecord(S->e_aux, S->aux));
-  // fact: Gram -> Cholesky / L^-1
-  rc = gp_gram_ardse(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, S->fact);
-  if (rc) return rc;
-  rc = gp_potrf_inv(G, n, ldg, strideG, Linv, ldinv, strideInv, batch, info, logdet, S->fact);
-  if (rc) return rc;
-  GP_CK(hipEventRecord(S->e_fact, S->fact));
   // pred: z, then TRMM + mean / var chunk by chunk.  One launch per chunk (not one for all):
   // the dispatcher interleaves another stream's kernels between launches, so a concurrent
   // factorisation is not starved behind a 25 ms grid (measured: 14 ms vs 3 ms per potrf).
