@@ -197,11 +197,20 @@ class EmulatorModel:
         np.savez(path if path.endswith(".npz") else path + ".npz", **arrs)
 
     def restore_model_info(self, path):
+        """Read ``path + '.npz'`` written by save_model_info (or an export of a SEPIA fit with
+        ``samples_<name>`` arrays, in SEPIA's ``(S,) + val_shape`` layout or flattened)."""
         f = path if path.endswith(".npz") else path + ".npz"
+        samples = {}
         with np.load(f, allow_pickle=False) as z:
-            samples = {k[8:]: z[k] for k in z.files if k.startswith("samples_")}
             for k in z.files:
-                if k.startswith("param_"):
+                if k.startswith("samples_"):
+                    v = np.asarray(z[k], dtype=np.float64)
+                    name = k[8:]
+                    if name in ModelParams.names and v.ndim >= 1:
+                        # (S,) + val_shape -> (S, prod(val_shape)), C order (betaU (S, (d+1) P))
+                        v = v.reshape(v.shape[0], -1)
+                    samples[name] = v
+                elif k.startswith("param_"):
                     self.params[k[6:]] = z[k]
                 elif k.startswith("step_"):
                     p = getattr(self.params, k[5:])

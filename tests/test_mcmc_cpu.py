@@ -85,3 +85,20 @@ def test_oracle_chain_moves_and_respects_bounds():
     assert np.all(rec["lamUz"] >= 0.3) and np.all((rec["lamWs"] >= 60) & (rec["lamWs"] <= 1e5))
     assert np.all(rec["betaU"] >= 0)
     assert acc["lamUz"].sum() > 0 and acc["betaU"].sum() > 0
+
+
+def test_restore_accepts_sepia_shaped_samples(tmp_path):
+    """restore_model_info flattens SEPIA's (S,) + val_shape sample arrays (npz export)."""
+    from gladsgp_amd.emulator import EmulatorModel
+    S, d, P = 5, 3, 2
+    rng = np.random.default_rng(0)
+    bu = rng.random((S, d + 1, P))
+    f = tmp_path / "m.npz"
+    np.savez(f, samples_betaU=bu, samples_lamUz=rng.random((S, 1, P)),
+             samples_lamWs=rng.random((S, 1, P)), samples_lamWOs=rng.random(S))
+    m = EmulatorModel.__new__(EmulatorModel)       # I/O only: no data / device needed
+    m.params = mcmc.ModelParams(d, P)
+    m.restore_model_info(str(f))
+    assert m.samples["betaU"].shape == (S, (d + 1) * P)
+    np.testing.assert_array_equal(m.samples["betaU"].reshape(S, d + 1, P), bu)
+    assert m.samples["lamUz"].shape == (S, P) and m.samples["lamWOs"].shape == (S, 1)
