@@ -131,7 +131,9 @@ def main():
     ap.add_argument("--m-chunk", type=int, default=0)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds for the CPU leg")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=("c3", "c4"), default="c3")
+    ap.add_argument("--workload", choices=("c3", "c4", "fit"), default="c3")
+    ap.add_argument("--ny", type=int, default=1347945, help="fit: field size per run")
+    ap.add_argument("--fit-pcs", type=int, default=8, help="fit: principal components")
     ap.add_argument("--serial", action="store_true",
                     help="c3: one stream, no overlap at all (gram, potrf, predict in order)")
     ap.add_argument("--pipeline", action="store_true",
@@ -142,6 +144,8 @@ def main():
     args = ap.parse_args()
     if args.workload == "c4":
         return main_c4(args)
+    if args.workload == "fit":
+        return main_fit(args)
 
     ctx = gdist.init_from_env("cuda")
     dev = ctx.device
@@ -348,6 +352,69 @@ def main_c4(args):
         "cpu_baseline": None,
     }
     assert out is not None and out[0].shape == (P, m)
+    print(json.dumps(line), flush=True)
+
+
+# reference fit timings (timing.csv:9, n=512 P=8: PCA incl. load/standardise,
+# tune_step_sizes(100, 5) + do_mcmc(512))
+REF_FIT_PCA_S = 31.673
+REF_FIT_MCMC_S = 1405.595
+
+
+def main_fit(args):
+    """The reference's fit_models at its own timing configuration (src/model.py:152-245,
+    timing.csv:9): n=512 runs, d=8, a 1,347,945-node field (float32 like the reference), PCA
+    basis from randomized_svd(p=25), P=8 PC GPs, tune_step_sizes(100, 5) + do_mcmc(512).
+    One GPU; the model and timing files go to a temporary directory."""
+    import shutil
+    import tempfile
+    import types
+    from gladsgp_amd import model as gmodel
+    dev = torch.device("cuda", 0)
+    n, d, P, ny = 512, 8, args.fit_pcs, args.ny
+    rng = np.random.default_rng(0)
+    t = rng.random((n, d))
+    nm = 12
+    modes = (rng.standard_normal((nm, ny)) * (0.6 ** np.arange(nm))[:, None]).astype(np.float32)
+    coef = np.stack([np.sin(2 * np.pi * t @ rng.uniform(0, 1, d) + k) for k in range(nm)], 1)
+    Y = (coef.astype(np.float32) @ modes)
+    Y += 1e-3 * rng.standard_normal(Y.shape, dtype=np.float32)
+    tmp = tempfile.mkdtemp(prefix="gladsgp_fit_")
+    try:
+        np.savetxt(os.path.join(tmp, "X.csv"), t, delimiter=",",
+                   header=",".join(f"x{i}" for i in range(d)), comments="")
+        np.save(os.path.join(tmp, "Y.npy"), Y.T)          # the reference stores (ny, n)
+        del Y
+        cfg = types.SimpleNamespace(X_standard=os.path.join(tmp, "X.csv"),
+                                    Y_physical=os.path.join(tmp, "Y.npy"), data_dir=tmp,
+                                    exp="bench")
+        t0 = time.perf_counter()
+        gmodel.fit_models(cfg, [n], [P], dtype=np.float32, recompute=True, device=dev, seed=0)
+        torch.cuda.synchronize()
+        total = time.perf_counter() - t0
+        tim = np.loadtxt(os.path.join(tmp, "models", "timing.csv"), delimiter=",")
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    pca_s, mcmc_s = float(tim[2]), float(tim[3])
+    value = pca_s + mcmc_s
+    ref = REF_FIT_PCA_S + REF_FIT_MCMC_S if (P == 8 and ny == 1347945) else None
+    sweeps = 100 * 5 + 100 + 512      # burn-in + 5 tuning levels + samples
+    line = {
+        "metric": "GladsGP fit seconds (PCA + Metropolis MCMC), n=512 d=8 P=8 "
+                  "ny=1,347,945 (timing.csv:9)",
+        "value": value, "unit": "s", "n_gpus": 1, "steps": 1, "warmup": 0,
+        "ms_per_step": value * 1e3, "higher_is_better": False, "scaling": "strong",
+        "vs_baseline": (value / ref) if ref else None, "dtype": "f64",
+        "data": "synthetic low-rank field of the reference's shape (float32 in, like the "
+                "reference), seeded",
+        "config": {"workload": "fit_models: standardise + randomized_svd(p=25) + K basis + "
+                               "pc_prec + tune_step_sizes(100,5) + do_mcmc(512)",
+                   "n_train": n, "d": d, "pcs": P, "ny": ny},
+        "breakdown": {"pca_s": pca_s, "mcmc_s": mcmc_s, "ref_pca_s": REF_FIT_PCA_S,
+                      "ref_mcmc_s": REF_FIT_MCMC_S, "mcmc_ms_per_sweep": 1e3 * mcmc_s / sweeps,
+                      "wall_s": total},
+        "roofline": None, "cpu_baseline": None,
+    }
     print(json.dumps(line), flush=True)
 
 
