@@ -53,13 +53,24 @@ def _np(x):
     return x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
 
 
+def _to_device_f64(x, device) -> torch.Tensor:
+    """float64 device copy of ``x``: host arrays cross PCIe in their own dtype (float32
+    ensembles at half the bytes) and are widened on the device, not on the host."""
+    if torch.is_tensor(x):
+        return x.to(device=device, dtype=F64).contiguous()
+    a = np.ascontiguousarray(np.asarray(x))
+    if a.dtype not in (np.float32, np.float64):
+        a = a.astype(np.float64)
+    return torch.from_numpy(a).to(device).to(F64).contiguous()
+
+
 class SimData:
     """Simulation block: design, raw and standardised outputs, PCA basis (SEPIA sim_data)."""
 
     def __init__(self, t_sim, y_sim, y_ind_sim, device):
         self.device = device
-        self.t = torch.as_tensor(_np(t_sim), dtype=F64, device=device).contiguous()
-        self.y = torch.as_tensor(_np(y_sim), dtype=F64, device=device).contiguous()
+        self.t = _to_device_f64(t_sim, device)
+        self.y = _to_device_f64(y_sim, device)
         self.y_ind = np.asarray(y_ind_sim)
         self.y_mean = None
         self.y_sd = None
