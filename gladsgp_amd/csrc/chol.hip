@@ -34,6 +34,9 @@ namespace {
 
 constexpr int NB = 64;
 constexpr int LP = NB + 1;  // LDS pitch (doubles)
+#ifndef DIAG_PE
+#define DIAG_PE 4           // diag factor: steps between step-counter publications
+#endif
 
 struct __align__(16) Smem {
   double As[NB * LP];
@@ -260,7 +263,12 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
         w[j + 1] = fma(-readlane_f64(w[j + 1], j), t, w[j + 1]);
         M[j * NB + lane] = t;
         if constexpr (j + 2 < NB) bcast_axpy<j + 2>(w, &S[j * NB], t);
-        __hip_atomic_store((int*)&sm.step, j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // publish every DIAG_PE steps (and the last): the release store is a scheduling
+        // barrier, and between publications the next column's pivot chain can overlap this
+        // column's trailing FMAs
+        if constexpr ((j + 1) % DIAG_PE == 0 || j + 2 == NB)
+          __hip_atomic_store((int*)&sm.step, j + 1, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     });
     DIAG_STAMP(0, 1);
@@ -291,9 +299,8 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
     for (int r = 0; r < NB; ++r) bq[r] = (r == lane) ? 1.0 : 0.0;
     static_for<0, NB - 1, 1>([&](auto J) {
       constexpr int j = decltype(J)::value;
-      constexpr int PE = 4;   // poll wave 0's step counter every PE steps
-      if constexpr (j % PE == 0)
-        lds_wait_ge((int*)&sm.step, (j + PE < NB - 1) ? j + PE : NB - 1);
+      if constexpr (j % DIAG_PE == 0)   // wave 0 publishes every DIAG_PE steps
+        lds_wait_ge((int*)&sm.step, (j + DIAG_PE < NB - 1) ? j + DIAG_PE : NB - 1);
       bcast_axpy<j + 1>(bq, &M[j * NB], bq[j]);
     });
     DIAG_STAMP(1, 2);
