@@ -92,6 +92,22 @@ def test_argument_validation_returns_lapack_style_codes(lib):
     assert rc == -13  # workspace too small
     assert lib.gp_loglik(dummy, 0, 2, 2, dummy, 2, dummy, dummy, dummy, 0, 1, None, 0, dummy,
                          None, None) == 0
+    # gp_fit_predict: validated before anything is enqueued
+    assert lib.gp_fit_predict_ws_bytes(4096, 100000, 1, 0) >= lib.gp_predict_ws_bytes(4096,
+                                                                                       100000,
+                                                                                       1, 0)
+    args = [dummy, 2, dummy, 2, 100, 10, 2, dummy, 2, dummy, dummy, dummy, dummy, 100,
+            dummy, 100, 10000, dummy, 128, 128 * 128, None, None, dummy, dummy, 10, 1, dummy,
+            1 << 40, 0, None]
+    bad = list(args)
+    bad[10] = None                                   # delta
+    assert lib.gp_fit_predict(*bad) == -24
+    bad = list(args)
+    bad[15] = 50                                     # ldg < n
+    assert lib.gp_fit_predict(*bad) == -26
+    bad = list(args)
+    bad[27] = 16                                     # workspace too small
+    assert lib.gp_fit_predict(*bad) == -22
 
 
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):

@@ -271,3 +271,51 @@ def test_two_phase_predict_and_overlap_match_single(dev):
                                             _t(s, dev), _t(W, dev), m_chunk=1024)
     torch.cuda.synchronize()
     assert torch.equal(m1, m4) and torch.equal(v1, v4)
+
+
+@pytest.mark.parametrize("n,m,B", [(64, 700, 1), (129, 300, 2), (513, 5000, 3)])
+def test_fit_predict_edge_shapes(dev, n, m, B):
+    """gp_fit_predict == gram -> cholesky_inverse -> predict at odd sizes: one 64-block (the
+    cross-covariance starts at once), partial tiles, fewer test points than one chunk."""
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(n + m)
+    d = 5
+    X, Xs = rng.random((n, d)), rng.random((m, d))
+    betas = rng.uniform(0.5, 4, (B, d))
+    s = rng.uniform(0.5, 2, B)
+    delta = rng.uniform(1e-5, 1e-3, B)
+    W = rng.standard_normal((B, n))
+    Xd, Xsd = _t(X, dev), _t(Xs, dev)
+    ch = kernels.cholesky_inverse(kernels.gram(Xd, _t(betas, dev), _t(s, dev), _t(delta, dev)))
+    m1, v1 = kernels.predict(ch, Xd, Xsd, _t(betas, dev), _t(s, dev), _t(s, dev), _t(W, dev))
+    m2, v2, ch2 = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                      _t(s, dev), _t(W, dev))
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m2) and torch.equal(v1, v2)
+    assert torch.equal(ch.logdet, ch2.logdet)
+    for b in range(B):
+        ref_m, ref_v = gp_ref.predict(X, Xs, W[b], betas[b], s[b], delta[b])
+        np.testing.assert_allclose(m2[b].cpu().numpy(), ref_m, rtol=0,
+                                   atol=1e-8 * max(1.0, np.abs(ref_m).max()))
+        np.testing.assert_allclose(v2[b].cpu().numpy(), ref_v, rtol=0, atol=1e-9 * s[b])
+
+
+def test_fit_predict_reports_non_pd(dev):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(3)
+    n, m, d = 200, 1000, 3
+    X, Xs = rng.random((n, d)), rng.random((m, d))
+    betas = np.full((2, d), 1.0)
+    s = np.array([1.0, 1.0])
+    delta = np.array([1e-4, -3.0])          # problem 1 is indefinite
+    W = rng.standard_normal((2, n))
+    mean, var, ch = kernels.fit_predict(_t(X, dev), _t(Xs, dev), _t(betas, dev), _t(s, dev),
+                                        _t(delta, dev), _t(s, dev), _t(W, dev))
+    torch.cuda.synchronize()
+    info = ch.info.cpu().numpy()
+    assert info[0] == 0 and info[1] > 0
+    with pytest.raises(ValueError):
+        ch.check()
+    ref_m, _ = gp_ref.predict(X, Xs, W[0], betas[0], s[0], delta[0])
+    np.testing.assert_allclose(mean[0].cpu().numpy(), ref_m, rtol=0,
+                               atol=1e-8 * max(1.0, np.abs(ref_m).max()))
