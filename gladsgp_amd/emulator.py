@@ -314,6 +314,7 @@ class EmulatorPrediction:
                                        pred_nugget)
         S, P = s.shape
         self.S, self.m, self.P = S, Xs.shape[0], P
+        self.lamWOs = np.asarray(samples["lamWOs"], dtype=np.float64).reshape(S)
         units = [(a, j) for a in range(S) for j in range(P)]
         rank, world = (ctx.rank, ctx.world) if ctx is not None else (0, 1)
         mine = gdist.shard_units(len(units), rank, world)
@@ -357,8 +358,21 @@ class EmulatorPrediction:
         z = rng.standard_normal(self.w.shape)
         return self.w + np.sqrt(np.maximum(self.var, 0.0)) * z
 
-    def get_y(self, std: bool = False, w=None) -> np.ndarray:
-        """Field reconstruction y = (w K) sd + mu, shape (S, m, ny) — SEPIA get_y()."""
+    def error_draws(self, rng=None, per_point: bool = True) -> np.ndarray:
+        """Standardised residual error of the reference's predictions: one N(0, 1/sqrt(lamWOs_s))
+        draw per posterior sample s (``time_predictions.py:84-87``) or per (sample, test point)
+        (``per_point``, ``assess_all_models.py:493-497``), shape (S, m) / (S, 1).  The
+        reference scales it by sd_y in physical units; get_y(add_error=True) does the same."""
+        rng = np.random.default_rng() if rng is None else rng
+        cols = self.m if per_point else 1
+        return rng.standard_normal((self.S, cols)) / np.sqrt(self.lamWOs)[:, None]
+
+    def get_y(self, std: bool = False, w=None, add_error: bool = False, rng=None,
+              per_point: bool = True) -> np.ndarray:
+        """Field reconstruction y = (w K) sd + mu, shape (S, m, ny) — SEPIA get_y().
+
+        ``add_error`` adds the reference's PC-truncation error term (error_draws, times sd_y
+        in physical units): y = (w K + e) sd + mu, one scalar e per (sample[, point])."""
         sd_ = self.model.data.sim_data
         wd = self.w_dev if w is None else torch.as_tensor(w, dtype=F64,
                                                             device=self.model.device)
@@ -367,6 +381,10 @@ class EmulatorPrediction:
         Kc = CM.of_rowmajor(sd_.K)                               # (ny x P)
         Yc = gemm(False, False, Kc, Wc)                          # (ny x S m) = (w K)^T
         y = Yc.t[: S * m, : sd_.K.shape[1]]                      # (S m, ny) row-major
+        if add_error:
+            e = torch.as_tensor(self.error_draws(rng, per_point), dtype=F64, device=y.device)
+            e = e.expand(S, m) if e.shape[1] == 1 else e
+            y = y + e.reshape(S * m, 1)                          # one scalar per row
         if not std:
             y = blas.standardize(y.contiguous(), sd_.y_mean, sd_.y_sd, inverse=True)
         return y.reshape(S, m, -1).cpu().numpy()

@@ -98,6 +98,17 @@ def test_emulator_prediction_matches_restatement(dev, tmp_path):
     y_ref = gp_ref.reconstruct_y(pred.w, Kd, data.sim_data.y_mean.cpu().numpy(),
                                  data.sim_data.y_sd.cpu().numpy())
     np.testing.assert_allclose(pred.get_y(), y_ref, rtol=1e-10, atol=1e-10)
+    # + the reference's error term: sd_y * N(0, 1/sqrt(lamWOs_s)) per (sample, point)
+    # (assess_all_models.py:493-497) or per sample (time_predictions.py:84-87)
+    sd_y = data.sim_data.y_sd.cpu().numpy()
+    for per_point in (True, False):
+        e = pred.error_draws(np.random.default_rng(11), per_point=per_point)
+        ye = pred.get_y(add_error=True, rng=np.random.default_rng(11), per_point=per_point)
+        e3 = e[:, :, None] if per_point else e[:, None, :]
+        np.testing.assert_allclose(ye, y_ref + e3 * sd_y, rtol=1e-10, atol=1e-10)
+    z = pred.error_draws(np.random.default_rng(0), per_point=True)
+    assert z.shape == (S, 37)
+    np.testing.assert_allclose(np.std(z * np.sqrt(pred.lamWOs)[:, None]), 1.0, atol=0.3)
     # predictive nugget flag
     pred0 = EmulatorPrediction(model=model, samples=samples, t_pred=t_pred, pred_nugget=False)
     _, var0 = gp_ref.sepia_predict_w(t, t_pred, w_hat, samples, lam, pred_nugget=False)
