@@ -22,13 +22,6 @@
 #include "gpfit_internal.h"
 #include "../../include/gpfit.h"
 
-#ifdef GPFIT_DIAG_PROBE
-__device__ unsigned long long gpfit_diag_probe[8];
-#define DIAG_STAMP(w, k) \
-  do { if ((threadIdx.x & 63) == 0 && wv == (w)) gpfit_diag_probe[k] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define DIAG_STAMP(w, k) do { } while (0)
-#endif
 
 namespace {
 
@@ -240,12 +233,6 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
   lds_double* M = sm.Bs;
   if (tid == 0) sm.step = 0;
   __syncthreads();
-  DIAG_STAMP(0, 0);
-#if defined(GPFIT_DIAG_VARIANT) && GPFIT_DIAG_VARIANT == 3
-  if (tid == 0) sm.fail = 0;
-  __syncthreads();
-  return 0;
-#endif
   if (wv == 0) {
     double w[NB];
 #pragma unroll
@@ -271,7 +258,6 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
                              __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     });
-    DIAG_STAMP(0, 1);
     const double rs = rsqrt_nr(piv);
     sm.invs[lane] = rs;
     const bool badc = lane < nb && (!(piv > 0.0) || !isfinite(piv));
@@ -289,11 +275,6 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
     __syncthreads();
   } else if (wv == 1) {
     __syncthreads();
-#if defined(GPFIT_DIAG_VARIANT) && GPFIT_DIAG_VARIANT == 1
-    __syncthreads();
-    __syncthreads();
-    return 0;
-#endif
     double bq[NB];
 #pragma unroll
     for (int r = 0; r < NB; ++r) bq[r] = (r == lane) ? 1.0 : 0.0;
@@ -303,7 +284,6 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
         lds_wait_ge((int*)&sm.step, (j + DIAG_PE < NB - 1) ? j + DIAG_PE : NB - 1);
       bcast_axpy<j + 1>(bq, &M[j * NB], bq[j]);
     });
-    DIAG_STAMP(1, 2);
     __syncthreads();   // invs from wave 0; every M read done
 #pragma unroll
     for (int r = 0; r < NB; ++r) sm.Bs[r * LP + lane] = bq[r] * sm.invs[r];
@@ -312,7 +292,6 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
     __syncthreads();
   }
   __syncthreads();
-  DIAG_STAMP(0, 3);
   const int f = sm.fail;
   if (ld_out) *ld_out = sm.red[0];
   return f;

@@ -1,10 +1,9 @@
-// Timing probe for the Cholesky diagonal-block factor inside the real chol_diag_kernel:
-// gp_potrf_inv at n = 64 is exactly one chol_diag_kernel launch.  Built with GPFIT_DIAG_PROBE,
-// lane 0 of the named waves writes s_memtime stamps (sweep start, wave-0 sweep end, inverse
-// sweep end, exit).  Build/run: see tools/gpu_probe_diag.sh.
-#ifndef NOSTAMP
-#define GPFIT_DIAG_PROBE 1
-#endif
+// Timing + correctness probe for the Cholesky diagonal-block factor: gp_potrf_inv at n = 64 is
+// exactly one chol_diag_kernel launch.  Run under rocprofv3 --kernel-trace for the kernel's
+// duration (in-kernel s_memtime stamps were tried and distort the kernel's codegen).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form
+//        -Xclang -target-feature -Xclang +enable-ds128 tools/probe_diag.hip
+//        gladsgp_amd/csrc/profile.hip gladsgp_amd/csrc/gram.hip -o tools/probe_diag
 #include "../gladsgp_amd/csrc/chol.hip"
 #include <cstdio>
 #include <cmath>
@@ -26,7 +25,7 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int reps = 20;
-  double ev = 0, st[3] = {0, 0, 0};
+  double ev = 0;
   for (int r = 0; r < reps + 2; ++r) {
     hipMemcpy(dW, A.data(), n * n * 8, hipMemcpyHostToDevice);
     hipEventRecord(e0);
@@ -35,16 +34,7 @@ int main() {
     hipEventSynchronize(e1);
     float ms;
     hipEventElapsedTime(&ms, e0, e1);
-    unsigned long long s[8];
-#ifndef NOSTAMP
-    hipMemcpyFromSymbol(s, HIP_SYMBOL(gpfit_diag_probe), 64);
-#else
-    for (int k = 0; k < 8; ++k) s[k] = 0;
-#endif
-    if (r >= 2) {
-      ev += ms * 1e3 / reps;
-      for (int k = 0; k < 3; ++k) st[k] += (double)(s[k + 1] - s[0]) / reps;
-    }
+    if (r >= 2) ev += ms * 1e3 / reps;
   }
   hipMemcpy(L.data(), dW, n * n * 8, hipMemcpyDeviceToHost);
   std::vector<double> Xf(128 * 128);
@@ -58,8 +48,7 @@ int main() {
       e1m = fmax(e1m, fabs(s - A[i + j * n]));
       e2m = fmax(e2m, fabs(t - (i == j ? 1.0 : 0.0)));
     }
-  printf("potrf(64) call %.2f us (events, incl. memsets)  memtime ticks from sweep start: "
-         "wave-0 sweep %.0f  inverse sweep %.0f  exit %.0f\n", ev, st[0], st[1], st[2]);
+  printf("potrf(64) call %.2f us (events, incl. the memsets)\n", ev);
   printf("max |LL^T - A| = %.3e   max |Linv L - I| = %.3e\n", e1m, e2m);
   return 0;
 }
