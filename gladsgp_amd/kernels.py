@@ -310,9 +310,8 @@ def side_stream(device) -> torch.cuda.Stream:
 def fit_predict(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
                 workspace: PredictWorkspace | None = None, out=None):
     """Gram -> Cholesky/L^-1 -> predict for ``batch`` GPs in one gp_fit_predict call: the
-    cross-covariance and the TRMM of every finished 128-row tile of L^-1 run on a low-priority
-    library stream while the factorisation (high priority) continues.  Returns
-    (mean, var, chol)."""
+    cross-covariance runs on a library stream under the factorisation's latency-bound tail,
+    then the per-chunk TRMM + mean/var.  Returns (mean, var, chol)."""
     dev = X.device
     X = _as_f64(X, dev, "X")
     Xs = _as_f64(Xs, dev, "Xs")
