@@ -209,24 +209,27 @@ __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
   }
 }
 
+// mean / var of test points [j0, j0 + mv): column j's partial sums sit in chunk j / mc's slab
+// (slabs pslab doubles apart; pslab = 0 when every chunk reuses one slab).
 __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ part, int NI,
-                                                       int mc, int mv,
+                                                       int mc, long long pslab, int j0, int mv,
                                                        const double* __restrict__ s_pred,
                                                        double* __restrict__ mean,
-                                                       double* __restrict__ var, int ldo,
-                                                       int c0) {
+                                                       double* __restrict__ var, int ldo) {
   const int b = blockIdx.y;
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= mv) return;
-  const double* pm = part + (long long)(b * 2 + 0) * NI * mc + j;
-  const double* pv = part + (long long)(b * 2 + 1) * NI * mc + j;
+  const int jl = blockIdx.x * 256 + threadIdx.x;
+  if (jl >= mv) return;
+  const int j = j0 + jl, ch = j / mc, jj = j - ch * mc;
+  const double* pm = part + ch * pslab + (long long)(b * 2 + 0) * NI * mc + jj;
+  const double* pv = part + ch * pslab + (long long)(b * 2 + 1) * NI * mc + jj;
   double sm = 0.0, sv = 0.0;
+#pragma unroll 8
   for (int I = 0; I < NI; ++I) {
     sm += pm[(long long)I * mc];
     sv += pv[(long long)I * mc];
   }
-  mean[(long long)b * ldo + c0 + j] = sm;
-  var[(long long)b * ldo + c0 + j] = s_pred[b] - sv;
+  mean[(long long)b * ldo + j] = sm;
+  var[(long long)b * ldo + j] = s_pred[b] - sv;
 }
 
 template <int D>
@@ -267,11 +270,13 @@ int trmm_order() {
 
 struct Plan {
   int npad, NI, mc, NC, nchunks, slabs;
-  long long off_z, off_kt, off_part, bytes, slab_elems;
+  long long off_z, off_kt, off_part, bytes, slab_elems, part_elems;
 };
 
-// slabs = 1: one cross-covariance chunk at a time (gp_predict); slabs = nchunks: every chunk
-// materialised up front (gp_predict_cross + gp_predict_solve).
+// slabs = 1: one cross-covariance chunk and one partial-sum slab at a time (gp_predict, which
+// finalises each chunk after its TRMM); slabs = nchunks: every chunk's cross-covariance and
+// partial sums materialised (gp_predict_cross + gp_predict_solve, gp_fit_predict), so one
+// finalize launch after the last TRMM covers all m points.
 Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
   Plan p;
   p.npad = gp_padded_n(n);
@@ -297,7 +302,8 @@ Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
   p.slab_elems = (long long)batch * mc * p.npad;
   long long z = (long long)batch * p.npad;
   long long kt = p.slab_elems * p.slabs;
-  const long long part = (long long)batch * 2 * p.NI * mc;
+  p.part_elems = (long long)batch * 2 * p.NI * mc;
+  const long long part = p.part_elems * p.slabs;
   p.off_z = 0;
   p.off_kt = ((z * 8 + 255) / 256) * 256;
   p.off_part = p.off_kt + ((kt * 8 + 255) / 256) * 256;
@@ -379,21 +385,38 @@ hipError_t cross_chunk(const Plan& p, int ch, double* kt, const double* X, int l
   return e;
 }
 
-hipError_t solve_chunk(const Plan& p, int ch, const WS& w, const double* kt, const double* Linv,
-                       int ldinv, long long strideInv, int m, const double* s_pred,
-                       double* mean, double* var, int ldo, int batch, hipStream_t stream) {
+// TRMM of chunk ch into partial-sum slab `part`; with `fin`, also its mean / var.
+hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, const double* kt,
+                       const double* Linv, int ldinv, long long strideInv, int m,
+                       const double* s_pred, double* mean, double* var, int ldo, int batch,
+                       bool fin, hipStream_t stream) {
   const int c0 = ch * p.mc;
   const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
   const int ncol_tiles = gp_ceil_div(mv, BC);
   gpfit_prof_begin(GP_PROF_TRMM, stream);
   hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0, stream,
-                     Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, w.z, p.npad,
-                     w.part, p.NI, ncol_tiles, trmm_order());
+                     Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z, p.npad,
+                     part, p.NI, ncol_tiles, trmm_order());
   gpfit_prof_end(GP_PROF_TRMM, stream);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || !fin) return e;
   hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0, stream,
-                     w.part, p.NI, p.mc, mv, s_pred, mean, var, ldo, c0);
+                     part, p.NI, p.mc, 0LL, c0, mv, s_pred, mean, var, ldo);
+  return hipGetLastError();
+}
+
+// Every chunk's TRMM into its own slab, then one finalize over all m points.
+hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
+                     long long strideInv, int m, const double* s_pred, double* mean,
+                     double* var, int ldo, int batch, hipStream_t stream) {
+  for (int ch = 0; ch < p.nchunks; ++ch) {
+    hipError_t e = solve_chunk(p, ch, w.part + ch * p.part_elems, w.z,
+                               w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
+                               s_pred, mean, var, ldo, batch, false, stream);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(m, 256), batch), dim3(256), 0, stream,
+                     w.part, p.NI, p.mc, p.part_elems, 0, m, s_pred, mean, var, ldo);
   return hipGetLastError();
 }
 
@@ -421,8 +444,8 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
                           stream));
   for (int ch = 0; ch < p.nchunks; ++ch) {
     GP_CK(cross_chunk(p, ch, w.kt, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch, stream));
-    GP_CK(solve_chunk(p, ch, w, w.kt, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch,
-                      stream));
+    GP_CK(solve_chunk(p, ch, w.part, w.z, w.kt, Linv, ldinv, strideInv, m, s_pred, mean, var,
+                      ldo, batch, true, stream));
   }
 #undef GP_CK
   return 0;
@@ -467,9 +490,7 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
                           stream));
-  for (int ch = 0; ch < p.nchunks; ++ch)
-    GP_CK(solve_chunk(p, ch, w, w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
-                      s_pred, mean, var, ldo, batch, stream));
+  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, stream));
 #undef GP_CK
   return 0;
 }
@@ -580,9 +601,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   GP_CK(hipStreamWaitEvent(S->pred, S->e_aux, 0));
   GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
                           S->pred));
-  for (int ch = 0; ch < p.nchunks; ++ch)
-    GP_CK(solve_chunk(p, ch, w, w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
-                      s_pred, mean, var, ldo, batch, S->pred));
+  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, S->pred));
   GP_CK(hipEventRecord(S->e_done, S->pred));
   GP_CK(hipStreamWaitEvent(stream, S->e_done, 0));
 #undef GP_CK
