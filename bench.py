@@ -228,7 +228,7 @@ def main():
             "flop_per_launch": tr_flops / max(tr_cnt, 1),
             "work_note": "n^2 + 4n flop per prediction (lower-triangular L^-1 K*^T + mean/var)"}
     g_cnt, g_ms = prof["gram"]
-    g_bytes = (8.0 * n * n + 8.0 * n * d) * g_cnt
+    g_bytes = (4.0 * n * (n + 1) + 8.0 * n * d) * g_cnt   # lower triangle written + X read
     p_cnt, p_ms = prof["potrf"]
     p_flops = 2.0 * n ** 3 / 3.0 * p_cnt
     c_cnt, c_ms = prof["cross"]

@@ -18,3 +18,9 @@ constexpr int GPFIT_POTRF_NB = 64;   // column block of gp_potrf_inv (chol.hip N
 int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
                           int ldinv, long long strideInv, int batch, int* info, double* logdet,
                           hipStream_t stream, int k_ev, hipEvent_t ev);
+
+// gp_gram_ardse writing only the lower triangle (j <= i); the upper triangle is left untouched.
+// For callers that factorise the result right away (gram.hip).
+int gpfit_gram_lower(const double* X, int n, int d, int ldx, const double* beta, int ldbeta,
+                     const double* s, const double* delta, double* G, int ldg,
+                     long long strideG, int batch, hipStream_t stream);

@@ -24,11 +24,6 @@
 #include <mutex>
 #include <vector>
 
-hipError_t gpfit_ardse_launch(const double* XA, int na, int ldxa, const double* XB, int nb,
-                              int ldxb, int d, const double* beta, int ldbeta,
-                              const double* s, const double* delta, double* out, int ldo,
-                              long long stride_o, int rows_out, int cols_out, int batch,
-                              hipStream_t st);
 namespace {
 
 constexpr int BI = 128;   // V tile rows (L^-1 rows)
@@ -579,7 +574,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   GP_CK(hipEventRecord(S->e_start, stream));
   GP_CK(hipStreamWaitEvent(S->fact, S->e_start, 0));
   // fact: Gram -> Cholesky / L^-1, with e_late once the factorisation is latency-bound
-  rc = gp_gram_ardse(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, S->fact);
+  rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, S->fact);
   if (rc) return rc;
   const int nblk = gp_ceil_div(n, GPFIT_POTRF_NB);
   const int k_late = late_step(nblk);
