@@ -18,6 +18,7 @@
 // diag_factor_inv: barrier-free symmetric elimination in one wave's registers (L), with a
 // second wave applying the same row operations to I (L^-1); see the function.
 #include "gpfit_common.h"
+#include <cstdlib>
 #include "gpfit_profile.h"
 #include "gpfit_internal.h"
 #include "../../include/gpfit.h"
@@ -376,7 +377,70 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
   }
 }
 
+// One tile of the trailing update of step k (tile index idx over the T(T+1)/2 lower tiles of
+// A's trailing matrix, then the T(k+1) tiles of R): C -= opA * opB.
+struct UpdTile {
+  const double *Ap, *Bp;
+  double* Cp;
+  int ldb, ldc, rv, cv;
+  bool diag, trn;
+};
+
+GP_DEV UpdTile upd_tile(double* Ab, int lda, double* Xb, int ldx, int n, int k, int T, int idx) {
+  const int k0 = k * NB;
+  const int ntri = T * (T + 1) / 2;
+  UpdTile t;
+  if (idx < ntri) {
+    int ii = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+    while (ii * (ii + 1) / 2 > idx) --ii;
+    while ((ii + 1) * (ii + 2) / 2 <= idx) ++ii;
+    const int jj = idx - ii * (ii + 1) / 2;
+    const int i0 = (k + 1 + ii) * NB, j0 = (k + 1 + jj) * NB;
+    t.rv = min(NB, n - i0);
+    t.cv = min(NB, n - j0);
+    t.Ap = Ab + i0 + (long long)k0 * lda;               // L_ik
+    t.Bp = Ab + j0 + (long long)k0 * lda;               // L_jk  (opB[p][c] = L_jk(c,p), NAT)
+    t.ldb = lda;
+    t.trn = false;
+    t.Cp = Ab + i0 + (long long)j0 * lda;
+    t.ldc = lda;
+    t.diag = (ii == jj);
+  } else {
+    const int idx2 = idx - ntri;
+    const int ii = idx2 / (k + 1), c = idx2 % (k + 1);
+    const int i0 = (k + 1 + ii) * NB, c0 = c * NB;
+    t.rv = min(NB, n - i0);
+    t.cv = NB;
+    t.Ap = Ab + i0 + (long long)k0 * lda;               // L_ik
+    t.Bp = Xb + k0 + (long long)c0 * ldx;               // X_kc (opB[p][cc] = X(k0+p,c0+cc), TRN)
+    t.ldb = ldx;
+    t.trn = true;
+    t.Cp = Xb + i0 + (long long)c0 * ldx;
+    t.ldc = ldx;
+    t.diag = false;
+  }
+  return t;
+}
+
+// Global loads of one update tile into registers: the C tile (coalesced) and both operands.
+GP_DEV void upd_load(const UpdTile& t, int lda, int kv, OpTile& ta, OpTile& tb,
+                     double (&cpre)[16]) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    const bool ok = row < t.rv && col < t.cv && (!t.diag || row >= col);
+    cpre[q] = ok ? t.Cp[row + (long long)col * t.ldc] : 0.0;
+  }
+  load_op(ta, t.Ap, lda, t.rv, kv);
+  if (t.trn) load_op(tb, t.Bp, t.ldb, kv, NB);
+  else load_op(tb, t.Bp, t.ldb, t.cv, kv);
+}
+
 // Trailing update of step k.  Block 0 owns tile (k+1, k+1) and then factors it (lookahead).
+// Blocks 1.. walk the other tiles with stride gridDim.x - 1 (the host caps the grid at two
+// resident blocks per CU), loading the next tile's operands and C into registers while the
+// current tile's MFMAs run.
 __global__ __launch_bounds__(256, 2) void chol_update_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
     long long sX, int n, int k, int T, int* __restrict__ info, double* __restrict__ logdet) {
@@ -386,58 +450,63 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(
   const int k0 = k * NB, kv = min(NB, n - k0);
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
-  const int ntri = T * (T + 1) / 2;
+  const int nt = T * (T + 1) / 2 + T * (k + 1);
   const int idx = blockIdx.x;
-  double* Cp;
-  int ldc, rv, cv, ldb;
-  bool diag = false, trn;
-  const double *Ap, *Bp;
-  if (idx < ntri) {
-    int ii = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
-    while (ii * (ii + 1) / 2 > idx) --ii;
-    while ((ii + 1) * (ii + 2) / 2 <= idx) ++ii;
-    const int jj = idx - ii * (ii + 1) / 2;
-    const int i0 = (k + 1 + ii) * NB, j0 = (k + 1 + jj) * NB;
-    rv = min(NB, n - i0);
-    cv = min(NB, n - j0);
-    Ap = Ab + i0 + (long long)k0 * lda;                 // L_ik
-    Bp = Ab + j0 + (long long)k0 * lda;                 // L_jk  (opB[p][c] = L_jk(c,p), NAT)
-    ldb = lda;
-    trn = false;
-    Cp = Ab + i0 + (long long)j0 * lda;
-    ldc = lda;
-    diag = (ii == jj);
-  } else {
-    const int idx2 = idx - ntri;
-    const int ii = idx2 / (k + 1), c = idx2 % (k + 1);
-    const int i0 = (k + 1 + ii) * NB, c0 = c * NB;
-    rv = min(NB, n - i0);
-    cv = NB;
-    Ap = Ab + i0 + (long long)k0 * lda;                 // L_ik
-    Bp = Xb + k0 + (long long)c0 * ldx;                 // X_kc (opB[p][cc] = X(k0+p,c0+cc), TRN)
-    ldb = ldx;
-    trn = true;
-    Cp = Xb + i0 + (long long)c0 * ldx;
-    ldc = ldx;
-  }
-  // prefetch the C tile (coalesced) while the operands are staged
-  double cpre[16];
+  if (idx != 0) {
+    const int stride = gridDim.x - 1;
+    UpdTile t = upd_tile(Ab, lda, Xb, ldx, n, k, T, idx);
+    OpTile ta, tb;
+    double cpre[16], cnext[16];
+    upd_load(t, lda, kv, ta, tb, cpre);
+    for (int i = idx; i < nt; i += stride) {
+      __syncthreads();               // the previous tile's epilogue has read As
+      store_op<false>(sm.As, ta);
+      if (t.trn) store_op<true>(sm.Bs, tb);
+      else store_op<false>(sm.Bs, tb);
+      __syncthreads();
+      const int inext = i + stride;
+      UpdTile tn = t;
+      if (inext < nt) {              // uniform: next tile's loads overlap this tile's MFMAs
+        tn = upd_tile(Ab, lda, Xb, ldx, n, k, T, inext);
+        upd_load(tn, lda, kv, ta, tb, cnext);
+      }
+      f64x4 acc[2][2];
+      mma64(sm.As, sm.Bs, acc);
+      __syncthreads();
+      acc_to_lds(sm.As, acc);        // As[col][row] = product
+      __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    int row, col;
-    slot_rc(q, row, col);
-    const bool ok = row < rv && col < cv && (!diag || row >= col);
-    cpre[q] = ok ? Cp[row + (long long)col * ldc] : 0.0;
+      for (int q = 0; q < 16; ++q) {
+        int row, col;
+        slot_rc(q, row, col);
+        if (row < t.rv && col < t.cv && (!t.diag || row >= col))
+          t.Cp[row + (long long)col * t.ldc] = cpre[q] - sm.As[col * LP + row];
+      }
+      if (inext < nt) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cpre[q] = cnext[q];
+        t = tn;
+      }
+    }
+    return;
   }
-  if (trn) stage2<true>(sm.As, Ap, lda, rv, sm.Bs, Bp, ldb, NB, kv);
-  else stage2<false>(sm.As, Ap, lda, rv, sm.Bs, Bp, ldb, cv, kv);
+  // block 0: tile (k+1, k+1) (an A tile on the diagonal), then its factorisation
+  const UpdTile t = upd_tile(Ab, lda, Xb, ldx, n, k, T, 0);
+  const int rv = t.rv, cv = t.cv;
+  double cpre[16];
+  {
+    OpTile ta, tb;
+    upd_load(t, lda, kv, ta, tb, cpre);
+    store_op<false>(sm.As, ta);
+    store_op<false>(sm.Bs, tb);
+  }
   __syncthreads();
   f64x4 acc[2][2];
   mma64(sm.As, sm.Bs, acc);
   __syncthreads();
   acc_to_lds(sm.As, acc);      // As[col][row] = product
   __syncthreads();
-  if (idx == 0) {
+  {
     // tile (k+1, k+1): updated lower values -> symmetric [row][col] tile in As, then factor
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -461,20 +530,31 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(
     }
     __syncthreads();
     diag_block(sm, Ab, lda, Xb, ldx, n, k + 1, info, logdet, b);
-    return;
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    int row, col;
-    slot_rc(q, row, col);
-    if (row < rv && col < cv && (!diag || row >= col))
-      Cp[row + (long long)col * ldc] = cpre[q] - sm.As[col * LP + row];
   }
 }
 
 }  // namespace
 
 static_assert(GPFIT_POTRF_NB == NB, "gpfit_internal.h must match the blocking");
+
+// Grid of chol_update_kernel for nt tiles per problem: block 0 plus workers, capped at two
+// resident blocks per CU over the whole batch so every worker is resident and walks several
+// tiles (GPFIT_UPD_CAP overrides the cap; 0 = one block per tile).
+static int update_grid(int nt, int batch) {
+  static const int cap_all = [] {
+    if (const char* e = getenv("GPFIT_UPD_CAP")) return atoi(e);
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+    return 2 * ncu;
+  }();
+  if (cap_all <= 0) return nt;
+  int cap = cap_all / (batch > 0 ? batch : 1);
+  if (cap < 2) cap = 2;
+  return nt < cap ? nt : cap;
+}
 
 extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double* Linv,
                             int ldinv, long long strideInv, int batch, int* info,
@@ -524,7 +604,8 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
     }
     if (T > 0) {
       const int nt = T * (T + 1) / 2 + T * (k + 1);
-      hipLaunchKernelGGL(chol_update_kernel, dim3(nt, batch), dim3(256), 0, stream, A, lda,
+      hipLaunchKernelGGL(chol_update_kernel, dim3(update_grid(nt, batch), batch), dim3(256), 0,
+                         stream, A, lda,
                          strideA, Linv, ldinv, strideInv, n, k, T, info, logdet);
       GP_CK(hipGetLastError());
     }

@@ -181,8 +181,8 @@ extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* b
   if (ws_bytes < c.bytes) return -13;
   if (!ll) return -14;
   const int npad = gp_padded_n(n);
-  int rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, c.G, n, (long long)n * n, batch,
-                         stream);
+  int rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, c.G, n, (long long)n * n,
+                            batch, stream);
   if (rc) return rc;
   rc = gp_potrf_inv(c.G, n, n, (long long)n * n, c.Linv, npad, (long long)npad * npad, batch,
                     c.info, c.logdet, stream);

@@ -372,12 +372,8 @@ hipError_t cross_chunk(const Plan& p, int ch, double* kt, const double* X, int l
                        int ldbeta, const double* s, int batch, hipStream_t stream) {
   const int c0 = ch * p.mc;
   const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
-  gpfit_prof_begin(GP_PROF_CROSS, stream);
-  hipError_t e = cross_kp_launch(X, n, ldx, Xs + (long long)c0 * ldxs, mv, ldxs, d, beta,
-                                 ldbeta, s, kt, p.mc, p.npad, (long long)p.mc * p.npad, batch,
-                                 stream);
-  gpfit_prof_end(GP_PROF_CROSS, stream);
-  return e;
+  return cross_kp_launch(X, n, ldx, Xs + (long long)c0 * ldxs, mv, ldxs, d, beta, ldbeta, s, kt,
+                         p.mc, p.npad, (long long)p.mc * p.npad, batch, stream);
 }
 
 // TRMM of chunk ch into partial-sum slab `part`; with `fin`, also its mean / var.
@@ -388,11 +384,11 @@ hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, con
   const int c0 = ch * p.mc;
   const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
   const int ncol_tiles = gp_ceil_div(mv, BC);
-  gpfit_prof_begin(GP_PROF_TRMM, stream);
+  if (fin) gpfit_prof_begin(GP_PROF_TRMM, stream);
   hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0, stream,
                      Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z, p.npad,
                      part, p.NI, ncol_tiles, trmm_order());
-  gpfit_prof_end(GP_PROF_TRMM, stream);
+  if (fin) gpfit_prof_end(GP_PROF_TRMM, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !fin) return e;
   hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0, stream,
@@ -404,12 +400,16 @@ hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, con
 hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
                      long long strideInv, int m, const double* s_pred, double* mean,
                      double* var, int ldo, int batch, hipStream_t stream) {
+  // timing: one event pair spans the back-to-back TRMM launches (an event record between
+  // launches costs a few us of stream time each); gp_profile_read reports it per launch.
+  gpfit_prof_begin_n(GP_PROF_TRMM, stream, p.nchunks);
   for (int ch = 0; ch < p.nchunks; ++ch) {
     hipError_t e = solve_chunk(p, ch, w.part + ch * p.part_elems, w.z,
                                w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
                                s_pred, mean, var, ldo, batch, false, stream);
     if (e != hipSuccess) return e;
   }
+  gpfit_prof_end(GP_PROF_TRMM, stream);
   hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(m, 256), batch), dim3(256), 0, stream,
                      w.part, p.NI, p.mc, p.part_elems, 0, m, s_pred, mean, var, ldo);
   return hipGetLastError();
@@ -438,7 +438,9 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
   GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
                           stream));
   for (int ch = 0; ch < p.nchunks; ++ch) {
+    gpfit_prof_begin(GP_PROF_CROSS, stream);
     GP_CK(cross_chunk(p, ch, w.kt, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch, stream));
+    gpfit_prof_end(GP_PROF_CROSS, stream);
     GP_CK(solve_chunk(p, ch, w.part, w.z, w.kt, Linv, ldinv, strideInv, m, s_pred, mean, var,
                       ldo, batch, true, stream));
   }
@@ -458,11 +460,14 @@ extern "C" int gp_predict_cross(const double* X, int ldx, const double* Xs, int 
   if (!ws) return -21;
   if (ws_bytes < p.bytes) return -22;
   const WS w = carve(p, ws);
+  // one timing-event pair around all chunks (the stream runs nothing else in between)
+  gpfit_prof_begin_n(GP_PROF_CROSS, stream, p.nchunks);
   for (int ch = 0; ch < p.nchunks; ++ch) {
     hipError_t e = cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n,
                                m, d, beta, ldbeta, s, batch, stream);
     if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   }
+  gpfit_prof_end(GP_PROF_CROSS, stream);
   return 0;
 }
 
@@ -523,6 +528,14 @@ int late_step(int nblk) {
   const int k = (int)(f * nblk);
   return k < 0 ? 0 : k;
 }
+// CUs the cross-covariance stream leaves free (GPFIT_AUX_FREE_CUS, default 0).
+int aux_free_cus() {
+  static int v = [] {
+    const char* e = getenv("GPFIT_AUX_FREE_CUS");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 std::mutex g_fp_mu;
 FitPredictStreams g_fp[64];
 
@@ -534,9 +547,23 @@ hipError_t fit_predict_streams(FitPredictStreams** out) {
   std::lock_guard<std::mutex> lk(g_fp_mu);
   FitPredictStreams& S = g_fp[dev];
   if (!S.fact) {
-    hipStream_t* st[3] = {&S.fact, &S.aux, &S.pred};
-    for (hipStream_t* p : st)
-      if ((e = hipStreamCreateWithFlags(p, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&S.fact, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&S.pred, hipStreamNonBlocking)) != hipSuccess) return e;
+    // the cross-covariance stream may leave aux_free_cus() CUs to the factorisation it runs
+    // beside (logical CU i sits on XCD i % 8, tools/probe_cumask.hip: the low CUs are spread
+    // evenly over the XCDs)
+    const int fr = aux_free_cus();
+    int ncu = 0;
+    if (fr > 0 &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        fr < ncu) {
+      std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+      for (int i = fr; i < ncu; ++i) m[i / 32] |= 1u << (i % 32);
+      if ((e = hipExtStreamCreateWithCUMask(&S.aux, (uint32_t)m.size(), m.data())) != hipSuccess)
+        return e;
+    } else if ((e = hipStreamCreateWithFlags(&S.aux, hipStreamNonBlocking)) != hipSuccess) {
+      return e;
+    }
     hipEvent_t* ev[5] = {&S.e_start, &S.e_fact, &S.e_aux, &S.e_done, &S.e_late};
     for (hipEvent_t* p : ev)
       if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
@@ -585,9 +612,11 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   GP_CK(hipEventRecord(S->e_fact, S->fact));
   // aux: cross-covariance of every chunk, from the factorisation's latency-bound phase on
   GP_CK(hipStreamWaitEvent(S->aux, S->e_late, 0));
+  gpfit_prof_begin_n(GP_PROF_CROSS, S->aux, p.nchunks);   // one event pair, all chunks
   for (int ch = 0; ch < p.nchunks; ++ch)
     GP_CK(cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n, m, d,
                       beta, ldbeta, s, batch, S->aux));
+  gpfit_prof_end(GP_PROF_CROSS, S->aux);
   GP_CK(hipEventRecord(S->e_aux, S->aux));
   // pred: z, then TRMM + mean / var chunk by chunk.  One launch per chunk (not one for all):
   // the dispatcher interleaves another stream's kernels between launches, so a concurrent

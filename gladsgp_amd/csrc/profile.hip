@@ -13,6 +13,7 @@ namespace {
 
 struct Slot {
   std::vector<hipEvent_t> start, stop;
+  std::vector<int> launches;   // launches bracketed by each pair
   int used = 0;
 };
 
@@ -21,12 +22,15 @@ Slot g_slots[GP_PROF_NUM];
 
 }  // namespace
 
-void gpfit_prof_begin(int id, hipStream_t st) {
+void gpfit_prof_begin_n(int id, hipStream_t st, int launches) {
   if (!g_enabled || id < 0 || id >= GP_PROF_NUM) return;
   Slot& s = g_slots[id];
   if (s.used >= (int)s.start.size()) return;   // capacity exhausted: stop recording
+  s.launches[s.used] = launches > 0 ? launches : 1;
   (void)hipEventRecord(s.start[s.used], st);
 }
+
+void gpfit_prof_begin(int id, hipStream_t st) { gpfit_prof_begin_n(id, st, 1); }
 
 void gpfit_prof_end(int id, hipStream_t st) {
   if (!g_enabled || id < 0 || id >= GP_PROF_NUM) return;
@@ -43,6 +47,7 @@ extern "C" int gp_profile_enable(int capacity) {
     for (auto e : s.stop) (void)hipEventDestroy(e);
     s.start.clear();
     s.stop.clear();
+    s.launches.assign(capacity, 1);
     s.used = 0;
     for (int i = 0; i < capacity; ++i) {
       hipEvent_t a, b;
@@ -66,6 +71,7 @@ extern "C" int gp_profile_read(int id, int* count, double* total_ms, double* max
   if (id < 0 || id >= GP_PROF_NUM) return -1;
   Slot& s = g_slots[id];
   double tot = 0.0, mx = 0.0;
+  int cnt = 0;
   for (int i = 0; i < s.used; ++i) {
     hipError_t e = hipEventSynchronize(s.stop[i]);
     if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
@@ -73,9 +79,10 @@ extern "C" int gp_profile_read(int id, int* count, double* total_ms, double* max
     e = hipEventElapsedTime(&ms, s.start[i], s.stop[i]);
     if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
     tot += ms;
-    if (ms > mx) mx = ms;
+    cnt += s.launches[i];
+    if (ms / s.launches[i] > mx) mx = ms / s.launches[i];
   }
-  if (count) *count = s.used;
+  if (count) *count = cnt;
   if (total_ms) *total_ms = tot;
   if (max_ms) *max_ms = mx;
   return 0;

@@ -214,7 +214,11 @@ int gp_syevj(double* A, int r, int lda, double* W, double* V, int ldv, int max_s
  * Optional kernel timing (diagnostics; not part of the reference surface).  When enabled with
  * capacity > 0, instrumented launches record a hipEvent pair on their own stream; after the
  * stream has drained, gp_profile_read returns the number of recorded launches of kernel `id`
- * and their summed / largest device time in milliseconds.  Host-side, single-threaded use.
+ * and their summed / largest device time in milliseconds.  A run of back-to-back launches of
+ * one kernel on one stream (gp_fit_predict's and gp_predict_solve's TRMM chunks, the cross-
+ * covariance chunks) is bracketed by one pair and counted as that many launches, so the
+ * events do not add stream time between them; `max_ms` is then the largest per-launch mean of
+ * a run.  Host-side, single-threaded use.
  */
 #define GP_PROF_GRAM 0        /* gram / cross-covariance build (ardse_kernel)            */
 #define GP_PROF_POTRF 1       /* whole gp_potrf_inv sequence                             */

@@ -81,7 +81,7 @@ def test_cross_matches_oracle(dev):
     assert np.max(np.abs(Kt - ref)) <= 8 * EPS
 
 
-@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 127, 128, 129, 200, 512, 1000])
+@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 127, 128, 129, 200, 512, 1000, 2100])
 def test_cholesky_inverse(dev, n):
     from gladsgp_amd import kernels
     rng = np.random.default_rng(n)
@@ -130,6 +130,24 @@ def test_cholesky_info_not_pd(dev, n, bad):
     _, info_ref = gp_ref.cholesky(G)
     ch = kernels.cholesky_inverse(_t(G, dev).unsqueeze(0).contiguous())
     assert int(ch.info[0]) == info_ref == bad
+
+
+def test_cholesky_batch_persistent_update(dev):
+    """A batch large enough that the update grid is capped: workers walk several tiles."""
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(21)
+    n, B = 1100, 6
+    Gs = []
+    for b in range(B):
+        X = rng.random((n, 8))
+        Gs.append(gp_ref.gram_ardse(X, rng.uniform(0.5, 5, 8), 1.0, 1e-3))
+    ch = kernels.cholesky_inverse(_t(np.stack(Gs), dev).contiguous())
+    assert ch.info.cpu().tolist() == [0] * B
+    for b in range(B):
+        L = ch.L[b].cpu().numpy()
+        assert np.linalg.norm(L @ L.T - Gs[b]) / np.linalg.norm(Gs[b]) <= 1e-13
+        Linv = ch.Linv[b].cpu().numpy()
+        assert np.max(np.abs(Linv @ L - np.eye(n))) <= 1e-9
 
 
 def test_cholesky_batch_mixed_info(dev):
