@@ -515,24 +515,26 @@ struct FitPredictStreams {
 };
 
 // Block step of the n/64 blocked factorisation from which the HBM-bound cross-covariance runs
-// beside it.  Started at once it doubles the early (bandwidth-bound) trailing updates
-// (54 -> 123 us); started in the latency-bound tail it fills idle bandwidth.  Sweep at C3
-// (20 steps): start fraction 0 / 0.5 / 0.6 / 0.7 / 0.8 -> 30.2 / 29.85 / 29.78 / 29.85 /
-// 30.07 ms per step (later than ~0.7 the cross-covariance outlasts the factorisation).
-// GPFIT_CROSS_START (fraction of the steps, 0 = at once) overrides.
+// beside it.  On all CUs, started at once it doubled the early (bandwidth-bound) trailing
+// updates (54 -> 123 us) and 0.6 was best (30.2 / 29.85 / 29.78 / 29.85 / 30.07 ms at 0 / 0.5 /
+// 0.6 / 0.7 / 0.8); on the CU-masked stream (aux_free_cus) 0.25 is best.  GPFIT_CROSS_START
+// (fraction of the steps, 0 = at once) overrides.
 int late_step(int nblk) {
   static double f = [] {
     const char* e = getenv("GPFIT_CROSS_START");
-    return e ? atof(e) : 0.6;
+    return e ? atof(e) : 0.25;
   }();
   const int k = (int)(f * nblk);
   return k < 0 ? 0 : k;
 }
-// CUs the cross-covariance stream leaves free (GPFIT_AUX_FREE_CUS, default 0).
+// CUs the cross-covariance stream leaves free for the factorisation (GPFIT_AUX_FREE_CUS).
+// With 64 of 256 CUs reserved the cross-covariance can start early without stretching the
+// factorisation's latency-bound tail: C3 step 29.37 -> 29.13 ms together with a start at 25%
+// of the block steps (profiles/r01/ab_update_persistent_auxmask*.log; same-box A/B runs).
 int aux_free_cus() {
   static int v = [] {
     const char* e = getenv("GPFIT_AUX_FREE_CUS");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 64;
   }();
   return v;
 }
