@@ -10,6 +10,7 @@ our kernels share one runtime and one device context.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 
@@ -20,6 +21,7 @@ from ._build import LIB_PATH
 c_int, c_ll, c_void_p, c_double_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p
 
 GPFIT_ERR_HIP = -1000
+GPFIT_ERR_RCCL = -3000
 
 # name -> (restype, argtypes); pointers are passed as integers (tensor.data_ptr()).
 SIGNATURES = {
@@ -52,6 +54,7 @@ SIGNATURES = {
                                c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int,
                                c_void_p]),
+    "gp_fit_predict_release": (c_int, []),
     "gp_loglik_ws_bytes": (c_ll, [c_int, c_int]),
     "gp_loglik": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                           c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,
@@ -69,6 +72,12 @@ SIGNATURES = {
     "gp_rowscale": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "gp_syevj": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
                          ctypes.c_double, c_void_p, c_int, c_void_p]),
+    "gp_comm_available": (c_int, []),
+    "gp_comm_unique_id": (c_int, [c_void_p]),
+    "gp_comm_init": (c_int, [c_int, c_int, c_void_p, c_void_p]),
+    "gp_comm_destroy": (c_int, [c_void_p]),
+    "gp_bcast": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_void_p]),
+    "gp_gather": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_void_p]),
     "gp_profile_enable": (c_int, [c_int]),
     "gp_profile_reset": (c_int, []),
     "gp_profile_read": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
@@ -85,7 +94,9 @@ class GPFitError(RuntimeError):
     """A libgpfit entry point returned a non-zero status."""
 
     def __init__(self, func: str, rc: int):
-        if rc <= GPFIT_ERR_HIP:
+        if rc <= GPFIT_ERR_RCCL:
+            msg = f"{func}: RCCL error {GPFIT_ERR_RCCL - rc} (or librccl not loadable)"
+        elif rc <= GPFIT_ERR_HIP:
             msg = f"{func}: HIP error {GPFIT_ERR_HIP - rc}"
         else:
             msg = f"{func}: invalid argument #{-rc}"
@@ -115,7 +126,14 @@ def lib() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _LIB = handle
+    atexit.register(_release)    # runs before torch's own exit hooks (registered earlier)
     return handle
+
+
+def _release() -> None:
+    """Drop gp_fit_predict's library streams while the HIP runtime is still alive."""
+    if _LIB is not None and torch.cuda.is_initialized():
+        _LIB.gp_fit_predict_release()
 
 
 def call(name: str, *args) -> int:

@@ -576,6 +576,29 @@ hipError_t fit_predict_streams(FitPredictStreams** out) {
 
 }  // namespace
 
+extern "C" int gp_fit_predict_release(void) {
+  std::lock_guard<std::mutex> lk(g_fp_mu);
+  int dev0 = 0;
+  hipError_t e = hipGetDevice(&dev0);
+  if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  for (int dev = 0; dev < 64; ++dev) {
+    FitPredictStreams& S = g_fp[dev];
+    if (!S.fact) continue;
+    if ((e = hipSetDevice(dev)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+    hipStream_t st[3] = {S.fact, S.aux, S.pred};
+    for (hipStream_t x : st) {
+      if ((e = hipStreamSynchronize(x)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+      if ((e = hipStreamDestroy(x)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+    }
+    hipEvent_t ev[5] = {S.e_start, S.e_fact, S.e_aux, S.e_done, S.e_late};
+    for (hipEvent_t x : ev)
+      if ((e = hipEventDestroy(x)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+    S = FitPredictStreams{};
+  }
+  e = hipSetDevice(dev0);
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
 extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ldxs, int n,
                               int m, int d, const double* beta, int ldbeta, const double* s,
                               const double* delta, const double* s_pred, const double* w_hat,

@@ -108,3 +108,58 @@ def gather_rows(ctx: Context, local: torch.Tensor, counts: list[int]) -> torch.T
     if ctx.rank != 0:
         return None
     return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+
+
+class NativeComm:
+    """RCCL communicator owned by libgpfit (``gp_comm_*``, include/gpfit.h): the C-ABI route
+    for the one broadcast + one gather the sharded emulator needs.
+
+    The 128-byte RCCL id is made on rank 0 and travels over the existing torch.distributed
+    group (any backend); at world size 1 no group is needed.
+    """
+
+    def __init__(self, ctx: Context):
+        import ctypes
+
+        from . import _capi
+        self.ctx = ctx
+        if not _capi.lib().gp_comm_available():
+            raise _capi.GPFitUnavailable("librccl cannot be loaded: gp_comm_* unavailable")
+        uid = (ctypes.c_char * 128)()
+        if ctx.rank == 0:
+            _capi.call("gp_comm_unique_id", ctypes.addressof(uid))
+        if ctx.distributed:
+            dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+            t = torch.tensor(list(uid.raw), dtype=torch.uint8, device=dev)
+            dist.broadcast(t, src=0)
+            ctypes.memmove(uid, bytes(t.cpu().tolist()), 128)
+        self._handle = ctypes.c_void_p()
+        _capi.call("gp_comm_init", ctx.world, ctx.rank, ctypes.addressof(uid),
+                   ctypes.addressof(self._handle))
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.ctx.device).cuda_stream
+
+    def bcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        """In-place broadcast of a contiguous device tensor from ``root``."""
+        from . import _capi
+        assert t.is_cuda and t.is_contiguous()
+        _capi.call("gp_bcast", self._handle.value, t.data_ptr(), t.numel() * t.element_size(),
+                   root, self._stream())
+        return t
+
+    def gather(self, t: torch.Tensor, root: int = 0) -> torch.Tensor | None:
+        """Equal-shape tensors from every rank, stacked on ``root`` (None elsewhere)."""
+        from . import _capi
+        assert t.is_cuda and t.is_contiguous()
+        out = (torch.empty((self.ctx.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+               if self.ctx.rank == root else None)
+        _capi.call("gp_gather", self._handle.value, t.data_ptr(), t.numel() * t.element_size(),
+                   out.data_ptr() if out is not None else None, root, self._stream())
+        return out
+
+    def close(self) -> None:
+        from . import _capi
+        if self._handle.value:
+            _capi.call("gp_comm_destroy", self._handle.value)
+            self._handle.value = None

@@ -31,6 +31,7 @@ extern "C" {
 #endif
 
 #define GPFIT_ERR_HIP (-1000)
+#define GPFIT_ERR_RCCL (-3000)  /* gp_comm_*: GPFIT_ERR_RCCL - ncclResult_t; RCCL not loadable */
 #define GPFIT_MAX_DIM 32      /* largest input dimension d supported by the kernels      */
 #define GPFIT_TILE 128        /* row padding of the L^-1 buffer (predict MFMA tile edge) */
 
@@ -156,6 +157,14 @@ int gp_fit_predict(const double* X, int ldx, const double* Xs, int ldxs, int n, 
                    long long ws_bytes, int m_chunk, hipStream_t stream);
 
 /*
+ * Drain and destroy gp_fit_predict's library streams (on every device that has them); the
+ * next gp_fit_predict re-creates them.  The Python binding calls it at interpreter exit, while
+ * the HIP runtime is still up: the cross-covariance stream is CU-masked, and a masked queue
+ * left to the runtime's own teardown crashed the process exit under rocprofv3.
+ */
+int gp_fit_predict_release(void);
+
+/*
  * Batched GP log-likelihood in one stream-ordered call: Gram (gp_gram_ardse) -> Cholesky
  * (gp_potrf_inv) -> ll[b] = -(1/2 ||L_b^-1 w_b||^2 + 1/2 log|G_b|), no 2*pi term, with
  * ll[b] = -inf where the factorisation failed (info[b] != 0, optionally copied out to `info`).
@@ -209,6 +218,26 @@ int gp_rowscale(double* M, int rows, int cols, int ld, const double* f, int inv,
  * The r x r core of np.linalg.svd(B) in src/svd.py:63 (via B B^T). */
 int gp_syevj(double* A, int r, int lda, double* W, double* V, int ldv, int max_sweeps,
              double tol, int* sweeps, int want_sqrt, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * RCCL over xGMI for the sharded emulator: one communicator per process /
+ * GPU.  The (sample, PC) GPs are independent, so the only exchanges are one broadcast of the
+ * inputs (X, X*, w_hat, hyperparameters) from rank 0 and one gather of the (mean, var) shards
+ * to rank 0.  librccl is opened at run time (dlopen); where it cannot be loaded these return
+ * GPFIT_ERR_RCCL and the rest of the library is unaffected.  The reference has no distributed
+ * code: a C caller uses these instead of torch.distributed (gladsgp_amd.dist.NativeComm).
+ *   gp_comm_unique_id: rank 0 writes the 128-byte id every rank passes to gp_comm_init (the
+ *                      caller ships it out of band);
+ *   gp_bcast:          `bytes` from `root`'s buf to every rank's buf (stream-ordered);
+ *   gp_gather:         every rank's `bytes` at `send` land at recv + rank * bytes on `root`.
+ * ---------------------------------------------------------------------------------------- */
+int gp_comm_available(void);
+int gp_comm_unique_id(void* id128);
+int gp_comm_init(int nranks, int rank, const void* id128, void** comm);
+int gp_comm_destroy(void* comm);
+int gp_bcast(void* comm, void* buf, long long bytes, int root, hipStream_t stream);
+int gp_gather(void* comm, const void* send, long long bytes, void* recv, int root,
+              hipStream_t stream);
 
 /*
  * Optional kernel timing (diagnostics; not part of the reference surface).  When enabled with

@@ -110,6 +110,19 @@ def test_argument_validation_returns_lapack_style_codes(lib):
     assert lib.gp_fit_predict(*bad) == -22
 
 
+def test_comm_argument_validation(lib):
+    # RCCL wrappers: bad arguments are rejected before librccl is touched
+    dummy = ctypes.c_void_p(16)
+    assert lib.gp_comm_init(0, 0, dummy, dummy) == -1
+    assert lib.gp_comm_init(2, 2, dummy, dummy) == -2
+    assert lib.gp_comm_init(1, 0, None, dummy) == -3
+    assert lib.gp_comm_unique_id(None) == -1
+    assert lib.gp_bcast(None, dummy, 8, 0, None) == -1
+    assert lib.gp_gather(None, dummy, 8, dummy, 0, None) == -1
+    assert lib.gp_comm_destroy(None) == -1
+    assert lib.gp_comm_available() in (0, 1)
+
+
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     from gladsgp_amd import _capi
     monkeypatch.setattr(_capi, "_LIB", None)

@@ -170,3 +170,38 @@ def test_load_model_reference_layout(dev, tmp_path):
     data2, model2 = gm.load_model(cfg, 40, 2, device=dev)
     assert model2.samples is not None and model2.P == 2 and model2.n == 40
     np.testing.assert_array_equal(data2.sim_data.K.cpu().numpy(), data.sim_data.K.cpu().numpy())
+
+
+def test_c5_field_emulator(dev):
+    """n = 512 runs of a 10k-node field (smooth seeded function of the design
+    times fixed modes, + 1e-3 noise), a 64-PC basis from the GPU randomized_svd(Y_std, 64, k=0,
+    q=1) (plot_PC_RMSE.py:91's call), 64 PC GPs predicted for two posterior samples through
+    EmulatorPrediction; mean / variance checked against the oracle on the GPU's own basis."""
+    from gladsgp_amd.emulator import EmulatorData, EmulatorModel, EmulatorPrediction
+    from gladsgp_amd.svd import randomized_svd
+    rng = np.random.default_rng(55)
+    n, d, ny, P = 512, 8, 10000, 64
+    t = rng.random((n, d))
+    modes = rng.standard_normal((16, ny)) * (0.7 ** np.arange(16))[:, None]
+    coef = np.stack([np.sin(2 * np.pi * t @ rng.uniform(0, 1, d) + k) for k in range(16)], 1)
+    y = coef @ modes + 1e-3 * rng.standard_normal((n, ny))
+    data = EmulatorData(t, y, device=dev)
+    data.standardize_y()
+    np.random.seed(64)
+    U, S, Vh = randomized_svd(data.sim_data.y_std, P, k=0, q=1)
+    K = (S[:, None] * Vh / np.sqrt(n)).contiguous()
+    data.create_K_basis(K)
+    model = EmulatorModel(data)
+    assert model.P == P and model.w_hat.shape == (n, P)
+    samples = _samples(2, d, P, seed=56)
+    t_pred = rng.random((300, d))
+    pred = EmulatorPrediction(model=model, samples=samples, t_pred=t_pred)
+    assert pred.w.shape == (2, 300, P)
+    w_hat = model.w_hat.cpu().numpy()
+    lam = model.LamSim.cpu().numpy()
+    mean_r, var_r = gp_ref.sepia_predict_w(t, t_pred, w_hat, samples, lam)
+    np.testing.assert_allclose(pred.w, mean_r, atol=1e-9 * max(1, np.abs(mean_r).max()))
+    np.testing.assert_allclose(pred.var, var_r, atol=1e-10 * max(1, np.abs(var_r).max()))
+    # the oracle's PC weights for this basis agree with the GPU's (pinv(K), model.py:219)
+    ystd = data.sim_data.y_std.cpu().numpy()
+    np.testing.assert_allclose(w_hat, gp_ref.pc_weights(ystd, K.cpu().numpy()), atol=1e-7)

@@ -337,3 +337,19 @@ def test_fit_predict_reports_non_pd(dev):
     ref_m, _ = gp_ref.predict(X, Xs, W[0], betas[0], s[0], delta[0])
     np.testing.assert_allclose(mean[0].cpu().numpy(), ref_m, rtol=0,
                                atol=1e-8 * max(1.0, np.abs(ref_m).max()))
+
+
+def test_native_comm_world1(dev):
+    """gp_comm_* (RCCL C-ABI) at world size 1: broadcast leaves the buffer, gather stacks it."""
+    from gladsgp_amd import _capi
+    from gladsgp_amd import dist as gd
+    assert _capi.lib().gp_comm_available() == 1
+    ctx = gd.Context(0, 1, 0, dev, None)
+    comm = gd.NativeComm(ctx)
+    x = torch.arange(1000, dtype=torch.float64, device=dev)
+    comm.bcast_(x)
+    g = comm.gather(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, torch.arange(1000, dtype=torch.float64, device=dev))
+    assert g.shape == (1, 1000) and torch.equal(g[0], x)
+    comm.close()
