@@ -383,7 +383,7 @@ struct UpdTile {
   const double *Ap, *Bp;
   double* Cp;
   int ldb, ldc, rv, cv;
-  bool diag, trn;
+  bool diag, trn, full;   // full: 64 x 64 off-diagonal, 16-byte aligned (no per-element checks)
 };
 
 GP_DEV UpdTile upd_tile(double* Ab, int lda, double* Xb, int ldx, int n, int k, int T, int idx) {
@@ -419,12 +419,40 @@ GP_DEV UpdTile upd_tile(double* Ab, int lda, double* Xb, int ldx, int n, int k, 
     t.ldc = ldx;
     t.diag = false;
   }
+  t.full = t.rv == NB && t.cv == NB && !t.diag && ((lda | t.ldb | t.ldc) & 1) == 0 &&
+           ((((size_t)t.Ap) | ((size_t)t.Bp)) & 15) == 0;
   return t;
 }
 
+// load_op's full-tile walk with one 64-bit step per slot (the worker's hot path).
+GP_DEV void load_full(OpTile& o, const double* __restrict__ src, int ld) {
+  const int tid = threadIdx.x;
+  const double* p = src + (tid & 31) * 2 + (long long)(tid >> 5) * ld;
+  const long long step = 8LL * ld;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const double2 x = *reinterpret_cast<const double2*>(p + q * step);
+    o.v[2 * q] = x.x;
+    o.v[2 * q + 1] = x.y;
+  }
+}
+
 // Global loads of one update tile into registers: the C tile (coalesced) and both operands.
+// Full tiles take a branch-free path: the code a cold instruction cache has to stream per
+// launch is what bounds these short kernels (tools/probe_update.hip: a worker's first tile
+// 22 us, its second 7 us).
 GP_DEV void upd_load(const UpdTile& t, int lda, int kv, OpTile& ta, OpTile& tb,
                      double (&cpre)[16]) {
+  const int tid = threadIdx.x;
+  if (t.full) {
+    const double* c = t.Cp + (tid & 63) + (long long)(tid >> 6) * t.ldc;
+    const long long cs = 4LL * t.ldc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) cpre[q] = c[q * cs];
+    load_full(ta, t.Ap, lda);
+    load_full(tb, t.Bp, t.ldb);
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     int row, col;
@@ -437,10 +465,35 @@ GP_DEV void upd_load(const UpdTile& t, int lda, int kv, OpTile& ta, OpTile& tb,
   else load_op(tb, t.Bp, t.ldb, t.cv, kv);
 }
 
+// C = cpre - product (product in Cs[col][row]), branch-free for full tiles.
+GP_DEV void upd_store(const UpdTile& t, const double (&cpre)[16], const double* Cs) {
+  const int tid = threadIdx.x;
+  if (t.full) {
+    const int row = tid & 63, col = tid >> 6;
+    double* c = t.Cp + row + (long long)col * t.ldc;
+    const long long cs = 4LL * t.ldc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) c[q * cs] = cpre[q] - Cs[(col + 4 * q) * LP + row];
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    if (row < t.rv && col < t.cv && (!t.diag || row >= col))
+      t.Cp[row + (long long)col * t.ldc] = cpre[q] - Cs[col * LP + row];
+  }
+}
+
 // Trailing update of step k.  Block 0 owns tile (k+1, k+1) and then factors it (lookahead).
 // Blocks 1.. walk the other tiles with stride gridDim.x - 1 (the host caps the grid at two
 // resident blocks per CU), loading the next tile's operands and C into registers while the
 // current tile's MFMAs run.
+// MODE (timing probe, tools/probe_update.hip): 0 = production, 1 = block 0 skips its factor,
+// 2 = block 0 only, 6 = workers return at once, 8 = as 1 with each worker's start / end
+// s_memrealtime written to logdet[2 idx], logdet[2 idx + 1], 9 = as 8 but the workers walk
+// their tiles twice and the stamps bracket the second pass (warm instruction cache).
+template <int MODE = 0>
 __global__ __launch_bounds__(256, 2) void chol_update_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
     long long sX, int n, int k, int T, int* __restrict__ info, double* __restrict__ logdet) {
@@ -452,41 +505,48 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(
   double* Xb = X + b * sX;
   const int nt = T * (T + 1) / 2 + T * (k + 1);
   const int idx = blockIdx.x;
+  const unsigned long long t_start = MODE >= 8 ? __builtin_amdgcn_s_memrealtime() : 0;
+  if ((MODE == 2 || MODE == 6) && idx != 0) return;
   if (idx != 0) {
+    // one call site each for the loads, the MFMAs, the epilogue and the LDS stores (compact
+    // code), software-pipelined: tile i's loads are issued before tile i - stride's MFMAs
     const int stride = gridDim.x - 1;
-    UpdTile t = upd_tile(Ab, lda, Xb, ldx, n, k, T, idx);
-    OpTile ta, tb;
-    double cpre[16], cnext[16];
-    upd_load(t, lda, kv, ta, tb, cpre);
-    for (int i = idx; i < nt; i += stride) {
-      __syncthreads();               // the previous tile's epilogue has read As
-      store_op<false>(sm.As, ta);
-      if (t.trn) store_op<true>(sm.Bs, tb);
-      else store_op<false>(sm.Bs, tb);
-      __syncthreads();
-      const int inext = i + stride;
-      UpdTile tn = t;
-      if (inext < nt) {              // uniform: next tile's loads overlap this tile's MFMAs
-        tn = upd_tile(Ab, lda, Xb, ldx, n, k, T, inext);
-        upd_load(tn, lda, kv, ta, tb, cnext);
-      }
-      f64x4 acc[2][2];
-      mma64(sm.As, sm.Bs, acc);
-      __syncthreads();
-      acc_to_lds(sm.As, acc);        // As[col][row] = product
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        int row, col;
-        slot_rc(q, row, col);
-        if (row < t.rv && col < t.cv && (!t.diag || row >= col))
-          t.Cp[row + (long long)col * t.ldc] = cpre[q] - sm.As[col * LP + row];
-      }
-      if (inext < nt) {
+    unsigned long long t_pass = t_start;
+    for (int pass = 0; pass < (MODE == 9 ? 2 : 1); ++pass) {
+      if (MODE == 9) t_pass = __builtin_amdgcn_s_memrealtime();
+      OpTile ta, tb;
+      double cpre[16], cnext[16];
+      UpdTile cur, prev;
+      bool started = false;
+      for (int i = idx;; i += stride) {
+        const bool have = i < nt;                       // uniform
+        if (have) {
+          cur = upd_tile(Ab, lda, Xb, ldx, n, k, T, i);
+          upd_load(cur, lda, kv, ta, tb, cnext);
+        }
+        if (started) {
+          f64x4 acc[2][2];
+          mma64(sm.As, sm.Bs, acc);
+          __syncthreads();
+          acc_to_lds(sm.As, acc);                       // As[col][row] = product
+          __syncthreads();
+          upd_store(prev, cpre, sm.As);
+        }
+        if (!have) break;
+        __syncthreads();                                // the epilogue has read As
+        store_op<false>(sm.As, ta);
+        if (cur.trn) store_op<true>(sm.Bs, tb);
+        else store_op<false>(sm.Bs, tb);
+        __syncthreads();
 #pragma unroll
         for (int q = 0; q < 16; ++q) cpre[q] = cnext[q];
-        t = tn;
+        prev = cur;
+        started = true;
       }
+    }
+    if ((MODE == 8 || MODE == 9) && threadIdx.x == 0) {
+      logdet[2 * idx] = (double)t_pass;
+      logdet[2 * idx + 1] = (double)__builtin_amdgcn_s_memrealtime();
     }
     return;
   }
@@ -529,7 +589,7 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(
       }
     }
     __syncthreads();
-    diag_block(sm, Ab, lda, Xb, ldx, n, k + 1, info, logdet, b);
+    if (MODE == 0 || MODE == 2) diag_block(sm, Ab, lda, Xb, ldx, n, k + 1, info, logdet, b);
   }
 }
 
@@ -604,7 +664,7 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
     }
     if (T > 0) {
       const int nt = T * (T + 1) / 2 + T * (k + 1);
-      hipLaunchKernelGGL(chol_update_kernel, dim3(update_grid(nt, batch), batch), dim3(256), 0,
+      hipLaunchKernelGGL(chol_update_kernel<0>, dim3(update_grid(nt, batch), batch), dim3(256), 0,
                          stream, A, lda,
                          strideA, Linv, ldinv, strideInv, n, k, T, info, logdet);
       GP_CK(hipGetLastError());
