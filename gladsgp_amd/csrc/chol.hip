@@ -73,6 +73,19 @@ GP_DEV void load_op(OpTile& t, const double* __restrict__ src, int ld, int fv, i
   }
 }
 
+// load_op's full-tile walk with one 64-bit step per slot (the worker's hot path).
+GP_DEV void load_full(OpTile& o, const double* __restrict__ src, int ld) {
+  const int tid = threadIdx.x;
+  const double* p = src + (tid & 31) * 2 + (long long)(tid >> 5) * ld;
+  const long long step = 8LL * ld;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const double2 x = *reinterpret_cast<const double2*>(p + q * step);
+    o.v[2 * q] = x.x;
+    o.v[2 * q + 1] = x.y;
+  }
+}
+
 template <bool TRN>
 GP_DEV void store_op(double* S, const OpTile& t) {
   const int tid = threadIdx.x;
@@ -88,18 +101,6 @@ GP_DEV void store_op(double* S, const OpTile& t) {
       S[(f + 1) * LP + sl] = t.v[2 * q + 1];
     }
   }
-}
-
-// As <- op A (NAT, x < av, k < kv), Bs <- op B (NAT or TRN, x < bv, k < kv)
-template <bool TRNB>
-GP_DEV void stage2(double* As, const double* __restrict__ A, int lda, int av, double* Bs,
-                   const double* __restrict__ B, int ldb, int bv, int kv) {
-  OpTile ta, tb;
-  load_op(ta, A, lda, av, kv);
-  if (!TRNB) load_op(tb, B, ldb, bv, kv);
-  else load_op(tb, B, ldb, kv, bv);
-  store_op<false>(As, ta);
-  store_op<TRNB>(Bs, tb);
 }
 
 // acc (this wave's 32x32) = sum_k As[k][rows] * Bs[k][cols]
@@ -142,20 +143,6 @@ GP_DEV void slot_rc(int q, int& row, int& col) {
   const int g = threadIdx.x + 256 * q;
   row = g & (NB - 1);
   col = g >> 6;
-}
-
-// C = acc (STORE) for rows < rv, cols < cv.
-GP_DEV void store_tile(double* Cs, const f64x4 (&acc)[2][2], double* __restrict__ C, int ld,
-                       int rv, int cv) {
-  __syncthreads();  // all waves done with As/Bs (Cs aliases As)
-  acc_to_lds(Cs, acc);
-  __syncthreads();
-#pragma unroll 4
-  for (int q = 0; q < 16; ++q) {
-    int row, col;
-    slot_rc(q, row, col);
-    if (row < rv && col < cv) C[row + (long long)col * ld] = Cs[col * LP + row];
-  }
 }
 
 using LdsSmem = __attribute__((address_space(3))) Smem;
@@ -357,23 +344,68 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
   const double* Dk = Xb + k0 + (long long)k0 * ldx;   // D_k = X_kk (lower, zero upper)
-  f64x4 acc[2][2];
-  if ((int)blockIdx.x < nbelow) {
-    // L_ik = A_ik D_k^T :  opA[r][p] = A_ik(r,p) (NAT), opB[p][c] = D_k(c,p) (NAT)
-    const int i0 = (k + 1 + blockIdx.x) * NB, rv = min(NB, n - i0);
-    double* Aik = Ab + i0 + (long long)k0 * lda;
-    stage2<false>(sm.As, Aik, lda, rv, sm.Bs, Dk, ldx, kv, kv);
-    __syncthreads();
-    mma64(sm.As, sm.Bs, acc);
-    store_tile(sm.As, acc, Aik, lda, rv, kv);
+  // both tile kinds through one code path (a short kernel's cost is largely the code a cold
+  // instruction cache streams, see upd_load):
+  //   L_ik = A_ik D_k^T : opA = A_ik (NAT, rv rows), opB[p][c] = D_k(c,p) (NAT), C = A_ik
+  //   X_kc = D_k R_kc   : opA = D_k (NAT),          opB[p][c] = R_kc(p,c) (TRN), C = R_kc
+  const bool lt = (int)blockIdx.x < nbelow;
+  const double *pa, *pb;
+  double* pc;
+  int la, av, rv, cv;
+  if (lt) {
+    const int i0 = (k + 1 + blockIdx.x) * NB;
+    rv = min(NB, n - i0);
+    cv = kv;
+    pc = Ab + i0 + (long long)k0 * lda;
+    pa = pc;
+    la = lda;
+    av = rv;
+    pb = Dk;
   } else {
-    // X_kc = D_k R_kc :  opA[r][p] = D_k(r,p) (NAT), opB[p][c] = R_kc(p,c) (TRN)
     const int c0 = (blockIdx.x - nbelow) * NB;
-    double* Rkc = Xb + k0 + (long long)c0 * ldx;
-    stage2<true>(sm.As, Dk, ldx, kv, sm.Bs, Rkc, ldx, NB, kv);
-    __syncthreads();
-    mma64(sm.As, sm.Bs, acc);
-    store_tile(sm.As, acc, Rkc, ldx, kv, NB);
+    rv = kv;
+    cv = NB;
+    pc = Xb + k0 + (long long)c0 * ldx;
+    pa = Dk;
+    la = ldx;
+    av = kv;
+    pb = pc;
+  }
+  const int ld_c = lt ? lda : ldx;
+  OpTile ta, tb;
+  const bool full = rv == NB && cv == NB && kv == NB && ((lda | ldx) & 1) == 0 &&
+                    ((((size_t)pa) | ((size_t)pb)) & 15) == 0;
+  if (full) {
+    load_full(ta, pa, la);
+    load_full(tb, pb, ldx);
+  } else {
+    load_op(ta, pa, la, av, kv);
+    if (lt) load_op(tb, pb, ldx, kv, kv);
+    else load_op(tb, pb, ldx, kv, NB);
+  }
+  store_op<false>(sm.As, ta);
+  if (lt) store_op<false>(sm.Bs, tb);
+  else store_op<true>(sm.Bs, tb);
+  __syncthreads();
+  f64x4 acc[2][2];
+  mma64(sm.As, sm.Bs, acc);
+  __syncthreads();
+  acc_to_lds(sm.As, acc);
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (full) {
+    const int row = tid & 63, col = tid >> 6;
+    double* c = pc + row + (long long)col * ld_c;
+    const long long cs = 4LL * ld_c;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) c[q * cs] = sm.As[(col + 4 * q) * LP + row];
+  } else {
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      int row, col;
+      slot_rc(q, row, col);
+      if (row < rv && col < cv) pc[row + (long long)col * ld_c] = sm.As[col * LP + row];
+    }
   }
 }
 
@@ -422,19 +454,6 @@ GP_DEV UpdTile upd_tile(double* Ab, int lda, double* Xb, int ldx, int n, int k, 
   t.full = t.rv == NB && t.cv == NB && !t.diag && ((lda | t.ldb | t.ldc) & 1) == 0 &&
            ((((size_t)t.Ap) | ((size_t)t.Bp)) & 15) == 0;
   return t;
-}
-
-// load_op's full-tile walk with one 64-bit step per slot (the worker's hot path).
-GP_DEV void load_full(OpTile& o, const double* __restrict__ src, int ld) {
-  const int tid = threadIdx.x;
-  const double* p = src + (tid & 31) * 2 + (long long)(tid >> 5) * ld;
-  const long long step = 8LL * ld;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const double2 x = *reinterpret_cast<const double2*>(p + q * step);
-    o.v[2 * q] = x.x;
-    o.v[2 * q + 1] = x.y;
-  }
 }
 
 // Global loads of one update tile into registers: the C tile (coalesced) and both operands.
