@@ -266,12 +266,14 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
     double bq[NB];
 #pragma unroll
     for (int r = 0; r < NB; ++r) bq[r] = (r == lane) ? 1.0 : 0.0;
+#ifndef DIAG_PROBE_NO_INV   // tools/probe_diag.hip only: time wave 0's sweep alone
     static_for<0, NB - 1, 1>([&](auto J) {
       constexpr int j = decltype(J)::value;
       if constexpr (j % DIAG_PE == 0)   // wave 0 publishes every DIAG_PE steps
         lds_wait_ge((int*)&sm.step, (j + DIAG_PE < NB - 1) ? j + DIAG_PE : NB - 1);
       bcast_axpy<j + 1>(bq, &M[j * NB], bq[j]);
     });
+#endif
     __syncthreads();   // invs from wave 0; every M read done
 #pragma unroll
     for (int r = 0; r < NB; ++r) sm.Bs[r * LP + lane] = bq[r] * sm.invs[r];
