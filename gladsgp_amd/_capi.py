@@ -118,7 +118,7 @@ def lib() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -m gladsgp_amd._build` "
             "(or __graft_entry__.build()); there is no CPU fallback")
     try:
-        handle = ctypes.CDLL(LIB_PATH)
+        handle = ctypes.CDLL(os.environ.get("GPFIT_LIB_AB", LIB_PATH))   # A/B builds
     except OSError as exc:  # pragma: no cover - environment specific
         raise GPFitUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
     for name, (res, args) in SIGNATURES.items():

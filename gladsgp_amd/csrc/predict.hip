@@ -95,6 +95,33 @@ GP_DEV void glds16(const double* g, double* l) {
                                    (void __attribute__((address_space(3)))*)l, 16, 0, 0);
 }
 
+// One staged K step (16 k) of a wave's 64x64 sub-tile.  TAIL: the step lies in the tile's
+// diagonal block of L^-1, where the wave's 16-row MFMA tile mi only meets nonzero L^-1 entries
+// when mi >= lo (lo = the step's offset into the wave's own 64-row diagonal, in 16-k steps).
+// The skipped products are exact zeros (L^-1 is zero above the diagonal), so the sums are
+// unchanged and the SIMD goes to the co-resident block's waves instead.
+template <bool TAIL>
+GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__ Bs,
+                       f64x4 (&acc)[4][4], int wr, int wc, int li, int lk, int lo) {
+#pragma unroll
+  for (int k4 = 0; k4 < BK / 4; ++k4) {
+    const int k = k4 * 4 + lk;
+    double a[4], bb[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+      if (!TAIL || mi >= lo) a[mi] = As[k * APITCH + wr * 64 + mi * 16 + li];
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj)
+      bb[nj] = Bs[((k >> 1) * BC + wc * 64 + nj * 16 + li) * 2 + (k & 1)];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      if (TAIL && mi < lo) continue;
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = mfma16x16x4(a[mi], bb[nj], acc[mi][nj]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
     const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt2,
     int mc, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
@@ -143,25 +170,32 @@ __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
   issue(0, smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
+  // K steps [0, s_diag) lie left of the tile's diagonal block (every product counts); the
+  // last BI/BK steps cross it, where each wave skips its 16-row MFMA tiles that only meet the
+  // zero upper triangle of L^-1 (3% of the TRMM's MFMAs at n = 4096).
+  // K steps [0, s_diag) lie left of the tile's diagonal block (every product counts); the
+  // last BI/BK steps cross it, where each wave skips its 16-row MFMA tiles that only meet the
+  // zero upper triangle of L^-1 (3% of the TRMM's MFMAs at n = 4096).
+  // Codegen note: the next-stage issue stays behind a branch the compiler cannot fold
+  // (nsteps laundered through an SGPR), so it remains its own basic block as in a single
+  // loop; with the branch folded away the scheduler moved the barrier and its vmcnt(0) wait
+  // up among the MFMAs and exposed the load latency every step (1.10 vs 1.01 ms per launch).
+  const int s_diag = nsteps - BI / BK;
+  int nst = nsteps;
+  asm volatile("" : "+s"(nst));
+  int s = 0;
+  for (; s < s_diag; ++s) {
     double* cur = smem + (s & 1) * STAGE;
-    if (s + 1 < nsteps) issue(s + 1, smem + ((s + 1) & 1) * STAGE);
-    const double* As = cur;
-    const double* Bs = cur + ASTAGE;
-#pragma unroll
-    for (int k4 = 0; k4 < BK / 4; ++k4) {
-      const int k = k4 * 4 + lk;
-      double a[4], bb[4];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = As[k * APITCH + wr * 64 + mi * 16 + li];
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj)
-        bb[nj] = Bs[((k >> 1) * BC + wc * 64 + nj * 16 + li) * 2 + (k & 1)];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = mfma16x16x4(a[mi], bb[nj], acc[mi][nj]);
-    }
+    if (s + 1 < nst) issue(s + 1, smem + ((s + 1) & 1) * STAGE);
+    trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (; s < nsteps; ++s) {
+    double* cur = smem + (s & 1) * STAGE;
+    if (s + 1 < nst) issue(s + 1, smem + ((s + 1) & 1) * STAGE);
+    const int lo = (s - s_diag) - 4 * wr;   // wave-uniform
+    if (lo < 4) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, lo);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
