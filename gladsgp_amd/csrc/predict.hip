@@ -173,9 +173,6 @@ __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
   // K steps [0, s_diag) lie left of the tile's diagonal block (every product counts); the
   // last BI/BK steps cross it, where each wave skips its 16-row MFMA tiles that only meet the
   // zero upper triangle of L^-1 (3% of the TRMM's MFMAs at n = 4096).
-  // K steps [0, s_diag) lie left of the tile's diagonal block (every product counts); the
-  // last BI/BK steps cross it, where each wave skips its 16-row MFMA tiles that only meet the
-  // zero upper triangle of L^-1 (3% of the TRMM's MFMAs at n = 4096).
   // Codegen note: the next-stage issue stays behind a branch the compiler cannot fold
   // (nsteps laundered through an SGPR), so it remains its own basic block as in a single
   // loop; with the branch folded away the scheduler moved the barrier and its vmcnt(0) wait
@@ -238,6 +235,114 @@ __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
   }
 }
 
+// Row-tile pairs: block (p, C) computes tile (NI-1-p, C) and then tile (p, C), so every block
+// runs 8(NI+1) K steps (uniform work: at C3 the 512 blocks of a chunk are exactly one
+// residency wave of 2 per CU, no tail) and the second tile's first stage is fetched under the
+// first tile's last MFMAs.  Loop bodies as in trmm_reduce_kernel.
+__global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
+    const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt2,
+    int mc, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
+    int NI, int NC) {
+  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
+  const int b = blockIdx.y;
+  const int p = blockIdx.x / NC, C = blockIdx.x % NC;
+  const int Ihi = NI - 1 - p, Ilo = p;
+  const int npass = (Ihi == Ilo) ? 1 : 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
+  const double* Lb = Linv + b * sL + 2 * lane;                          // + I*BI + k*ld
+  const double* K = Kt2 + b * sK + ((long long)C * BC) * 2 + 2 * lane; // + (kp*mc)*2 (+128)
+
+  auto issue = [&](const double* L, int s, double* st) {
+    const int k0 = s * BK;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {              // A rows k0 + 4w + r
+      const int kr = 4 * w + r;
+      glds16(L + (long long)(k0 + kr) * ld, st + kr * APITCH);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {              // B: k-pair 2w + (r >> 1), half r & 1
+      const int kpl = 2 * w + (r >> 1), h = r & 1;
+      glds16(K + ((long long)(k0 / 2 + kpl) * mc) * 2 + h * 128,
+             st + ASTAGE + kpl * 256 + h * 128);
+    }
+  };
+
+  issue(Lb + Ihi * BI, 0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll 1
+  for (int pass = 0; pass < npass; ++pass) {
+    const int I = pass ? Ilo : Ihi;
+    const double* L = Lb + I * BI;
+    const int nsteps = (I + 1) * (BI / BK);   // even: the last step reads stage buffer 1
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[a][c] = zero4();
+    const int s_diag = nsteps - BI / BK;
+    int nst = nsteps;
+    asm volatile("" : "+s"(nst));
+    int s = 0;
+    for (; s < s_diag; ++s) {
+      double* cur = smem + (s & 1) * STAGE;
+      if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
+      trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (; s < nsteps; ++s) {
+      double* cur = smem + (s & 1) * STAGE;
+      if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
+      else if (pass + 1 < npass) issue(Lb + Ilo * BI, 0, smem);   // next tile's first stage
+      const int lo = (s - s_diag) - 4 * wr;   // wave-uniform
+      if (lo < 4) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, lo);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+
+    // epilogue in stage buffer 1 (buffer 0 may hold the next tile's first stage)
+    double* red = smem + STAGE;
+    const double* zb = z + (long long)b * npad + I * BI + wr * 64;
+    double zr[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zr[mi][r] = zb[mi * 16 + lk + 4 * r];
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      double sm = 0.0, sv = 0.0;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double v = acc[mi][nj][r];
+          sm = fma(v, zr[mi][r], sm);
+          sv = fma(v, v, sv);
+        }
+      sm += __shfl_xor(sm, 16, 64);
+      sv += __shfl_xor(sv, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (lk == 0) {
+        red[(wr * 2 + 0) * BC + wc * 64 + nj * 16 + li] = sm;
+        red[(wr * 2 + 1) * BC + wc * 64 + nj * 16 + li] = sv;
+      }
+    }
+    __syncthreads();
+    if (tid < BC) {
+      const int col = C * BC + tid;
+      double* pm = part + ((long long)(b * 2 + 0) * NI + I) * mc;
+      double* pv = part + ((long long)(b * 2 + 1) * NI + I) * mc;
+      pm[col] = red[0 * BC + tid] + red[2 * BC + tid];
+      pv[col] = red[1 * BC + tid] + red[3 * BC + tid];
+    }
+    __syncthreads();   // red (buffer 1) is read before the next tile's step 0 refills it
+  }
+}
+
 // mean / var of test points [j0, j0 + mv): column j's partial sums sit in chunk j / mc's slab
 // (slabs pslab doubles apart; pslab = 0 when every chunk reuses one slab).
 __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ part, int NI,
@@ -295,6 +400,17 @@ int trmm_order() {
     return e ? atoi(e) : 0;
   }();
   return v;
+}
+
+// Row-tile pairs per block (trmm_pair_kernel, the default) or one tile per block in the
+// GPFIT_TRMM_ORDER dispatch order (GPFIT_TRMM_PAIR=0).  Same-box A/B: C4 (n = 1024) 2.226 ->
+// 2.122 ms per launch, C3 1.002-1.008 -> 1.001-1.003 (profiles/r01/ab_trmm_pair.log).
+bool trmm_pair() {
+  static const int v = [] {
+    const char* e = getenv("GPFIT_TRMM_PAIR");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
 }
 
 struct Plan {
@@ -419,9 +535,14 @@ hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, con
   const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
   const int ncol_tiles = gp_ceil_div(mv, BC);
   if (fin) gpfit_prof_begin(GP_PROF_TRMM, stream);
-  hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0, stream,
-                     Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z, p.npad,
-                     part, p.NI, ncol_tiles, trmm_order());
+  if (trmm_pair())
+    hipLaunchKernelGGL(trmm_pair_kernel, dim3((p.NI + 1) / 2 * ncol_tiles, batch), dim3(256), 0,
+                       stream, Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z,
+                       p.npad, part, p.NI, ncol_tiles);
+  else
+    hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0, stream,
+                       Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z, p.npad,
+                       part, p.NI, ncol_tiles, trmm_order());
   if (fin) gpfit_prof_end(GP_PROF_TRMM, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !fin) return e;
