@@ -20,7 +20,7 @@ setup, the PCs are dealt round-robin to ranks, each step ends with one gather of
 rank's (mean, var) rows to rank 0 (strong scaling: total work fixed).
 
 rank 0 prints ONE JSON line with the metric, a roofline object for the dominant kernel
-(trmm_reduce, timed live with HIP events on its own stream via gp_profile_*), auxiliary
+(trmm_pair_kernel, timed live with HIP events on its own stream via gp_profile_*), auxiliary
 rooflines, and a CPU baseline (the numpy fp64 oracle on the host cores, bounded sample).
 """
 from __future__ import annotations
@@ -141,6 +141,10 @@ def main():
                          "under the current TRMM (measured no gain: the TRMM holds every CU "
                          "slot and the factorisation's launches wait behind it)")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
+    ap.add_argument("--c4-path", choices=("fit_predict", "predict"), default="predict",
+                    help="c4: gram -> potrf -> gp_predict (default), or one gp_fit_predict per "
+                         "step (measured 1-3%% slower at C4: its cross-covariance, 5x the "
+                         "batched potrf, stretches the potrf and the TRMM waits for all of it)")
     args = ap.parse_args()
     if args.workload == "c4":
         return main_c4(args)
@@ -219,9 +223,10 @@ def main():
     tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
     if os.path.exists(tf) and n == 4096 and args.m_chunk in (0, 4096):
         tj = json.load(open(tf))
-        traffic = tj["kernels"]["trmm_reduce_kernel"]["bytes_per_launch"]
+        kt = tj["kernels"].get("trmm_pair_kernel") or tj["kernels"]["trmm_reduce_kernel"]
+        traffic = kt["bytes_per_launch"]
         traffic_src = "profiles/r01/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
-    roof = {"kernel": "trmm_reduce_kernel", "bound": "mfma", "achieved": round(tr_tfs, 3),
+    roof = {"kernel": "trmm_pair_kernel", "bound": "mfma", "achieved": round(tr_tfs, 3),
             "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": traffic_src, "launches": tr_cnt,
@@ -304,7 +309,12 @@ def main_c4(args):
     var = torch.empty((bl, m), dtype=torch.float64, device=dev)
 
     def step():
-        if bl:
+        if bl and args.c4_path == "fit_predict":
+            # one gp_fit_predict over this rank's PCs: the cross-covariance of every chunk runs
+            # on a library stream under the batched factorisation
+            kernels.fit_predict(Xd, Xsd, Bl, Sl, Dl, Sl, Wl, m_chunk=args.m_chunk, workspace=ws,
+                                out=(mean, var))
+        elif bl:
             G = kernels.gram(Xd, Bl, Sl, Dl, batch=bl)
             ch = kernels.cholesky_inverse(G)
             kernels.predict(ch, Xd, Xsd, Bl, Sl, Sl, Wl, m_chunk=args.m_chunk, workspace=ws,
@@ -343,8 +353,9 @@ def main_c4(args):
         "config": {"workload": "C4 multivariate emulator: per-PC Gram + Cholesky/L^-1 + "
                                "predict, gather to rank 0",
                    "pcs": P, "n_train": n, "m_test": m, "d": d,
-                   "parallelism": f"PC shards x{ctx.world} (RCCL broadcast + gather)"},
-        "roofline": {"kernel": "trmm_reduce_kernel (rank 0's PCs)", "bound": "mfma",
+                   "parallelism": f"PC shards x{ctx.world} (RCCL broadcast + gather)",
+                   "path": args.c4_path},
+        "roofline": {"kernel": "trmm_pair_kernel (rank 0's PCs)", "bound": "mfma",
                      "achieved": round(tr_tfs, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
                      "traffic": None, "launches": tr_cnt,
