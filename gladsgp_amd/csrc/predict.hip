@@ -9,8 +9,8 @@
 // both; V is reduced in registers and never written.
 //
 // Per chunk of m_c test points:
-//   1. cross_kp           Kt = s exp(-sum beta (X - Xs)^2), n_pad x m_c, stored k-pair
-//                         interleaved for the TRMM's LDS image (exp once per element)
+//   1. cross_kp           Kt = s exp(-sum beta (X - Xs)^2), n_pad x m_c, k-major rows of m_c
+//                         test points (the TRMM's LDS image row by row; exp once per element)
 //   2. trmm_reduce        for each 128x128 tile (I, C) of V: acc = sum_{k < 128(I+1)} X[I,k] Kt[k,C]
 //                         on v_mfma_f64_16x16x4_f64, epilogue: per-column partial sums of
 //                         acc*z and acc^2 -> part[b][I][col]  (MFMA-bound: n^2 m flop)
@@ -32,11 +32,11 @@ constexpr int BK = 16;    // K step
 constexpr long long kDefaultChunkElems = 256ll << 20;  // <= 2 GB of Kt per chunk
 constexpr int kDefaultChunk = 4096;                   // test points per chunk
 
-// Cross-covariance chunk in the k-pair-interleaved layout the TRMM streams:
-//   Kt2[((k >> 1) * mc + c) * 2 + (k & 1)] = s * exp(-sum beta (X[k] - Xs[c])^2)
+// Cross-covariance chunk, k-major as the TRMM streams it:
+//   Kt[k * mc + c] = s * exp(-sum beta (X[k] - Xs[c])^2)
 // (zero for k >= n or c >= mv).  Each thread owns one test point c (registers) and walks 32
-// k-pairs whose design rows are broadcast from LDS; it stores one 16-B pair per k-pair, so a
-// wave writes 1 KB contiguous per instruction.
+// k-pairs whose design rows are broadcast from LDS; a wave stores 512 contiguous bytes per
+// row k.
 template <int D>
 __global__ __launch_bounds__(256) void cross_kp_kernel(
     const double* __restrict__ X, int n, int ldx, const double* __restrict__ Xs, int mv,
@@ -74,7 +74,8 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
     double2 v;
     v.x = (col_ok && k < n) ? sb * exp(-e0) : 0.0;
     v.y = (col_ok && k + 1 < n) ? sb * exp(-e1) : 0.0;
-    *reinterpret_cast<double2*>(o + ((long long)(kp0 + kk) * mc + c) * 2) = v;
+    o[(long long)k * mc + c] = v.x;
+    o[(long long)(k + 1) * mc + c] = v.y;
   }
 }
 
@@ -82,8 +83,10 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
 // Operands stream straight into LDS with global_load_lds (16 B per lane), double-buffered:
 //   A step (16 k x 128 rows of L^-1): 16 rows of 1 KB, row pitch 1152 B (lanes 0-15 / 16-31
 //     of a fragment read land 32 banks apart: conflict-free)
-//   B step (8 k-pairs x 128 test points x 2): 2 KB per k-pair, already in the [kp][c][2]
-//     order of cross_kp_kernel, so a fragment read covers 256 contiguous bytes.
+//   B step (16 k x 128 test points): 16 rows of 1 KB, the k-major rows of cross_kp_kernel, so
+//     each 16-lane group of a fragment read covers 128 contiguous bytes (conflict-free; the
+//     earlier k-pair-interleaved image put lanes li and li + 8 on one bank: 33% of LDS cycles
+//     were bank conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE).
 // One barrier per K-step; ~69 KB of LDS and <= 256 VGPRs -> 2 blocks (8 waves) per CU.
 constexpr int APITCH = 144;                    // doubles per staged A row (1152 B)
 constexpr int ASTAGE = BK * APITCH;            // 2304 doubles
@@ -112,7 +115,7 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
       if (!TAIL || mi >= lo) a[mi] = As[k * APITCH + wr * 64 + mi * 16 + li];
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj)
-      bb[nj] = Bs[((k >> 1) * BC + wc * 64 + nj * 16 + li) * 2 + (k & 1)];
+      bb[nj] = Bs[k * BC + wc * 64 + nj * 16 + li];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       if (TAIL && mi < lo) continue;
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
   const double* L = Linv + b * sL + I * BI + 2 * lane;                 // + k*ld per row
-  const double* K = Kt2 + b * sK + ((long long)C * BC) * 2 + 2 * lane; // + (kp*mc)*2 (+128)
+  const double* K = Kt2 + b * sK + (long long)C * BC + 2 * lane;       // + k*mc per row
   const int nsteps = (I + 1) * (BI / BK);
 
   auto issue = [&](int s, double* st) {
@@ -154,10 +157,9 @@ __global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
       glds16(L + (long long)(k0 + kr) * ld, st + kr * APITCH);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {              // B: k-pair 2w + (r >> 1), half r & 1
-      const int kpl = 2 * w + (r >> 1), h = r & 1;
-      glds16(K + ((long long)(k0 / 2 + kpl) * mc) * 2 + h * 128,
-             st + ASTAGE + kpl * 256 + h * 128);
+    for (int r = 0; r < 4; ++r) {              // B rows k0 + 4w + r
+      const int kr = 4 * w + r;
+      glds16(K + (long long)(k0 + kr) * mc, st + ASTAGE + kr * BC);
     }
   };
 
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
   const double* Lb = Linv + b * sL + 2 * lane;                          // + I*BI + k*ld
-  const double* K = Kt2 + b * sK + ((long long)C * BC) * 2 + 2 * lane; // + (kp*mc)*2 (+128)
+  const double* K = Kt2 + b * sK + (long long)C * BC + 2 * lane;       // + k*mc per row
 
   auto issue = [&](const double* L, int s, double* st) {
     const int k0 = s * BK;
@@ -262,10 +264,9 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
       glds16(L + (long long)(k0 + kr) * ld, st + kr * APITCH);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {              // B: k-pair 2w + (r >> 1), half r & 1
-      const int kpl = 2 * w + (r >> 1), h = r & 1;
-      glds16(K + ((long long)(k0 / 2 + kpl) * mc) * 2 + h * 128,
-             st + ASTAGE + kpl * 256 + h * 128);
+    for (int r = 0; r < 4; ++r) {              // B rows k0 + 4w + r
+      const int kr = 4 * w + r;
+      glds16(K + (long long)(k0 + kr) * mc, st + ASTAGE + kr * BC);
     }
   };
 
