@@ -71,11 +71,11 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
       e0 = fma(bs[dd] * t0, t0, e0);
       e1 = fma(bs[dd] * t1, t1, e1);
     }
-    double2 v;
-    v.x = (col_ok && k < n) ? sb * exp(-e0) : 0.0;
-    v.y = (col_ok && k + 1 < n) ? sb * exp(-e1) : 0.0;
-    o[(long long)k * mc + c] = v.x;
-    o[(long long)(k + 1) * mc + c] = v.y;
+    // exp unconditionally, then select: padding rows / columns have finite (zeroed) inputs,
+    // and a conditional exp costs an exec-mask branch around each call
+    const double v0 = sb * exp(-e0), v1 = sb * exp(-e1);
+    o[(long long)k * mc + c] = (col_ok && k < n) ? v0 : 0.0;
+    o[(long long)(k + 1) * mc + c] = (col_ok && k + 1 < n) ? v1 : 0.0;
   }
 }
 
@@ -673,24 +673,28 @@ struct FitPredictStreams {
 // Block step of the n/64 blocked factorisation from which the HBM-bound cross-covariance runs
 // beside it.  On all CUs, started at once it doubled the early (bandwidth-bound) trailing
 // updates (54 -> 123 us) and 0.6 was best (30.2 / 29.85 / 29.78 / 29.85 / 30.07 ms at 0 / 0.5 /
-// 0.6 / 0.7 / 0.8); on the CU-masked stream (aux_free_cus) 0.25 is best.  GPFIT_CROSS_START
-// (fraction of the steps, 0 = at once) overrides.
+// 0.6 / 0.7 / 0.8); on the CU-masked stream (aux_free_cus) 0.25 was best, and 0.4 with 128
+// free CUs once the cross-covariance kernel stopped branching around its exps (it got faster
+// and leaned harder on the factorisation: profiles/r01/ab_cross_select_exp.log).
+// GPFIT_CROSS_START (fraction of the steps, 0 = at once) overrides.
 int late_step(int nblk) {
   static double f = [] {
     const char* e = getenv("GPFIT_CROSS_START");
-    return e ? atof(e) : 0.25;
+    return e ? atof(e) : 0.4;
   }();
   const int k = (int)(f * nblk);
   return k < 0 ? 0 : k;
 }
 // CUs the cross-covariance stream leaves free for the factorisation (GPFIT_AUX_FREE_CUS).
-// With 64 of 256 CUs reserved the cross-covariance can start early without stretching the
-// factorisation's latency-bound tail: C3 step 29.37 -> 29.13 ms together with a start at 25%
-// of the block steps (profiles/r01/ab_update_persistent_auxmask*.log; same-box A/B runs).
+// With CUs reserved the cross-covariance can start early without stretching the
+// factorisation's latency-bound tail: 64 reserved took the C3 step 29.37 -> 29.13 ms with a
+// start at 25% of the block steps (profiles/r01/ab_update_persistent_auxmask*.log); with the
+// faster, branch-free cross-covariance kernel 128 reserved and a start at 40% matched the old
+// kernel's C3 step while C4 (where it runs alone) gained 1.2%.
 int aux_free_cus() {
   static int v = [] {
     const char* e = getenv("GPFIT_AUX_FREE_CUS");
-    return e ? atoi(e) : 64;
+    return e ? atoi(e) : 128;
   }();
   return v;
 }
