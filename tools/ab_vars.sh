@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
 OUT=gpurun_out/ab_vars.log; : > $OUT
-for rep in 1 2; do for spec in "$@"; do
+for rep in $(seq 1 ${REPS:-2}); do for spec in "$@"; do
   tag=${spec%%:*}; vars=""; [ "$spec" != "$tag" ] && vars=$(echo "${spec#*:}" | tr ',' ' ')
   timeout -k 10 200 env GPFIT_X=0 $vars python bench.py --no-cpu --steps 10 --warmup 3 $BENCH_ARGS > gpurun_out/_ab.log 2>&1 || { echo "FAIL $tag" >> $OUT; tail -5 gpurun_out/_ab.log >> $OUT; cat $OUT; exit 1; }
   python3 - "$tag" >> $OUT <<'PY'
