@@ -103,7 +103,11 @@ GP_DEV void store_op(double* S, const OpTile& t) {
   }
 }
 
-// acc (this wave's 32x32) = sum_k As[k][rows] * Bs[k][cols]
+// acc (this wave's 32x32) = sum_k As[k][rows] * Bs[k][cols].  The MFMA's 4 k slots take rows
+// k4, k4+16, k4+32, k4+48 rather than 4 consecutive rows.  Measured: the factorisation inside
+// gp_fit_predict 3.47-3.49 -> 3.42-3.44 ms (same box, 3 reps, profiles/r01/ab_mma64_kslots.log);
+// the tiles' LDS bank-conflict share did not move (21%: it is the transposed tile stores, the
+// fragment reads are ds_read2_b64 and conflict-free either way).
 GP_DEV void mma64(const double* As, const double* Bs, f64x4 (&acc)[2][2]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
@@ -113,7 +117,7 @@ GP_DEV void mma64(const double* As, const double* Bs, f64x4 (&acc)[2][2]) {
     for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = zero4();
 #pragma unroll 4
   for (int k4 = 0; k4 < NB / 4; ++k4) {
-    const int k = k4 * 4 + lk;
+    const int k = k4 + (NB / 4) * lk;
     const double a0 = As[k * LP + wr * 32 + li], a1 = As[k * LP + wr * 32 + 16 + li];
     const double b0 = Bs[k * LP + wc * 32 + li], b1 = Bs[k * LP + wc * 32 + 16 + li];
     acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);

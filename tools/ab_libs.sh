@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
 OUT=gpurun_out/ab_libs.log; : > $OUT
-for rep in 1 2; do for tag in "$@"; do
+for rep in $(seq 1 ${REPS:-2}); do for tag in "$@"; do
   timeout -k 10 150 env GPFIT_LIB_AB=$PWD/_ab/lib_$tag.so python bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/_ab.log 2>&1 || { echo "FAIL $tag" >> $OUT; tail -5 gpurun_out/_ab.log >> $OUT; exit 1; }
   python3 - "$tag" >> $OUT <<'PY'
 import json, sys
