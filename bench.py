@@ -221,8 +221,9 @@ def main():
     tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    if os.path.exists(tf) and n == 4096 and args.m_chunk in (0, 4096):
-        tj = json.load(open(tf))
+    tj = json.load(open(tf)) if os.path.exists(tf) else {}
+    chunk = args.m_chunk or 16384   # the library's default test-point chunk for one GP
+    if tj and n == 4096 and chunk == tj.get("m_chunk"):
         kt = tj["kernels"].get("trmm_pair_kernel") or tj["kernels"]["trmm_reduce_kernel"]
         traffic = kt["bytes_per_launch"]
         traffic_src = "profiles/r01/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, per launch)"

@@ -30,7 +30,8 @@ constexpr int BI = 128;   // V tile rows (L^-1 rows)
 constexpr int BC = 128;   // V tile cols (test points)
 constexpr int BK = 16;    // K step
 constexpr long long kDefaultChunkElems = 256ll << 20;  // <= 2 GB of Kt per chunk
-constexpr int kDefaultChunk = 4096;                   // test points per chunk
+constexpr int kDefaultChunk = 4096;                   // test points per chunk (batches)
+constexpr int kDefaultChunkSingle = 16384;            // ... and for one GP
 
 // Cross-covariance chunk, k-major as the TRMM streams it:
 //   Kt[k * mc + c] = s * exp(-sum beta (X[k] - Xs[c])^2)
@@ -432,11 +433,15 @@ Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
   if (m_chunk > 0) {
     mc = gp_ceil_div(m_chunk, BC) * BC;
   } else {
-    // 4096 test points per chunk measured best at C3 and C4 (tools/sweep_trmm.sh); shrink
-    // only when the batch's cross-covariance slab would exceed kDefaultChunkElems doubles
+    // Test points per chunk: 4096 measured best for batches (C4, tools/job_c4chunk.sh) and
+    // 16384 for one GP (C3 with the row-pair TRMM: a launch is then 2048 blocks, four full
+    // residency waves; 28.51-28.59 vs 28.72-28.81 ms per step at 4096, 32768 slower:
+    // profiles/r01/sweep_c3_chunk_pair.log).  Shrunk only when the batch's cross-covariance
+    // slab would exceed kDefaultChunkElems doubles.
     long long cap = kDefaultChunkElems / ((long long)p.npad * (batch > 0 ? batch : 1));
     mc = (int)((cap / BC) * BC);
-    if (mc > kDefaultChunk) mc = kDefaultChunk;
+    const int def = batch == 1 ? kDefaultChunkSingle : kDefaultChunk;
+    if (mc > def) mc = def;
     if (mc < BC) mc = BC;
   }
   if (mc > mpad) mc = mpad;
