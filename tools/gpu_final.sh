@@ -18,3 +18,6 @@ timeout -k 10 120 rocprofv3 --kernel-trace -d $R/gpurun_out/potrf_tl -o run --ou
 python3 $R/tools/potrf_timeline.py $R/gpurun_out/potrf_tl/run_kernel_trace.csv > $R/gpurun_out/${TAG}_potrf_timeline.txt || exit 1
 bash $R/tools/pmc_traffic.sh > $R/gpurun_out/${TAG}_pmc.txt 2>&1 || exit 1
 tail -12 $R/gpurun_out/${TAG}_pmc.txt
+bash $R/tools/pmc_mfma.sh > $R/gpurun_out/${TAG}_pmc_mfma.txt 2>&1 || exit 1
+bash $R/tools/pmc_lds.sh > $R/gpurun_out/${TAG}_pmc_lds.txt 2>&1 || exit 1
+grep "trmm" $R/gpurun_out/${TAG}_pmc_mfma.txt $R/gpurun_out/${TAG}_pmc_lds.txt | cut -c1-200
