@@ -11,9 +11,10 @@
 // Per chunk of m_c test points:
 //   1. cross_kp           Kt = s exp(-sum beta (X - Xs)^2), n_pad x m_c, k-major rows of m_c
 //                         test points (the TRMM's LDS image row by row; exp once per element)
-//   2. trmm_reduce        for each 128x128 tile (I, C) of V: acc = sum_{k < 128(I+1)} X[I,k] Kt[k,C]
-//                         on v_mfma_f64_16x16x4_f64, epilogue: per-column partial sums of
-//                         acc*z and acc^2 -> part[b][I][col]  (MFMA-bound: n^2 m flop)
+//   2. trmm_pair          for each 128x128 tile (I, C) of V: acc = sum_{k < 128(I+1)} X[I,k] Kt[k,C]
+//                         on v_mfma_f64_16x16x4_f64 (row tiles NI-1-p and p in one block),
+//                         epilogue: per-column partial sums of acc*z and acc^2 ->
+//                         part[b][I][col]  (MFMA-bound: n^2 m flop)
 //   3. finalize           mean = sum_I pm, var = s_pred - sum_I pv
 // z = X w is a small lower-triangular gemv (linalg.hip trmv_kernel).
 #include "gpfit_common.h"
