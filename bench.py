@@ -5,14 +5,19 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step is one full pass of the hot path for one GP on one GPU, from hyperparameters to
-answers: ARD-SE Gram (n x n) -> blocked MFMA Cholesky + L^-1 -> fused cross-covariance /
-TRMM / mean+variance over that rank's m = 100k test points.  Within a step the
-cross-covariance (independent of the factorisation) is built on a second HIP stream while
-the latency-bound Cholesky runs (``--serial`` disables that); steps never overlap.  Inputs are HBM-resident before
-the timed region.  Ranks are independent test-point shards of one trained GP (weak scaling:
-every rank predicts its own 100k points; no collective inside a step), so
-value = N * 100k * K / max-over-ranks(time).
+A step is one full pass of the hot path for one GP, from hyperparameters to answers on rank 0:
+ARD-SE Gram (n x n) -> blocked MFMA Cholesky + L^-1 -> cross-covariance / TRMM / mean+variance
+over the test points.  Inside a step the cross-covariance (independent of the factorisation)
+runs on the caller-owned context's CU-masked stream while the latency-bound Cholesky runs
+(``--serial``: no context, every kernel in order on one stream).  Inputs are HBM-resident
+before the timed region.
+
+Multi-GPU (single-output GP): *strong scaling* of the fixed m = 100k test points.
+Rank r predicts the contiguous block ``shard_range(100000, r, N)``; every rank factorises the
+same n x n Gram redundantly (no exchange: the factorisation is the Amdahl term), and each step
+ends with one gather of every rank's (mean, var) rows to rank 0 (RCCL over xGMI), inside the
+timed region.  value = 100k * K / max-over-ranks(time).  The weak-scaled form (every rank its
+own 100k points, no collective) is reported beside it as ``weak`` when N > 1.
 
 ``--workload c4`` runs BASELINE config 4 instead (multivariate emulator: 32 independent PC
 GPs, n = 1024, m = 100k shared test points): rank 0 broadcasts the inputs over RCCL at
@@ -28,11 +33,21 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import platform
 import sys
 import time
 
-_CPU_THREADS = min(16, os.cpu_count() or 1)
+
+def _cpu_threads() -> int:
+    """Host threads for the CPU baseline: the pool's CPU share when it sets OMP_NUM_THREADS
+    (16 per GPU on the MI355X boxes, whose os.cpu_count() shows the whole machine), else every
+    CPU this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+_CPU_THREADS = _cpu_threads()
 for _v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS"):
     os.environ.setdefault(_v, str(_CPU_THREADS))
 
@@ -49,13 +64,13 @@ FP64_MFMA_PEAK_TFLOPS = 78.6    # MI355X dense FP64 matrix (spec); 70.1 measured
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E (spec); ~6300 achievable
 
 
-def c3_inputs(rank: int, n: int, m: int, d: int):
-    """SURVEY §8d C3 recipe (seeded).  Rank r predicts rows [r m, (r+1) m) of rng(2)'s stream."""
+def c3_inputs(n: int, m: int, d: int):
+    """SURVEY §8d C3 recipe (seeded): X = rng(0), a = rng(1), beta = rng(3), X* = rng(2)."""
     X = np.random.default_rng(0).random((n, d))
     a = np.random.default_rng(1).uniform(0, 1, d)
     y = np.sin(2 * np.pi * X @ a) + 0.1 * np.sum(X * X, axis=1)
     beta = np.random.default_rng(3).uniform(0.5, 5.0, d)
-    Xs = np.random.default_rng(2).random(((rank + 1) * m, d))[rank * m:]
+    Xs = np.random.default_rng(2).random((m, d))
     return X, y, beta, Xs, 1.0, 1e-6
 
 
@@ -68,29 +83,44 @@ def c4_inputs(n: int, m: int, d: int, P: int):
     return X, W, beta, Xs, np.ones(P), np.full(P, 1e-6)
 
 
-def cpu_baseline(X, y, beta, Xs, s, delta, budget_s: float):
-    """numpy fp64 oracle (Gram -> cholesky -> chunked cross-cov + solve_triangular) on host."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(X, y, beta, Xs, s, delta, sample: int = 20000, reps: int = 3):
+    """numpy fp64 oracle (Gram -> cholesky -> chunked cross-cov + solve_triangular) on the
+    host: full n = 4096 factorisation + prediction of the first ``sample`` test points, timed
+    ``reps`` times (median), extrapolated linearly in the test points to m."""
     from oracle import gp_ref
     import scipy.linalg as sla
-    t0 = time.perf_counter()
-    G = gp_ref.gram_ardse(X, beta, s, delta)
-    L = np.linalg.cholesky(G)
-    alpha = sla.cho_solve((L, True), y)
-    t_fact = time.perf_counter() - t0
-    chunk, done, t_pred = 2000, 0, 0.0
-    means, vars_ = [], []
-    while done < Xs.shape[0] and (t_fact + t_pred) < budget_s:
-        t1 = time.perf_counter()
-        Ks = gp_ref.cross_ardse(Xs[done:done + chunk], X, beta, s)
-        mu = Ks @ alpha
-        V = sla.solve_triangular(L, Ks.T, lower=True, check_finite=False)
-        var = s - np.einsum("ij,ij->j", V, V)
-        t_pred += time.perf_counter() - t1
-        means.append(mu)
-        vars_.append(var)
-        done += Ks.shape[0]
     m = Xs.shape[0]
-    t_full = t_fact + t_pred / done * m
+    sample = min(sample, m)
+    runs = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        G = gp_ref.gram_ardse(X, beta, s, delta)
+        L = np.linalg.cholesky(G)
+        alpha = sla.cho_solve((L, True), y)
+        t_fact = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        means, vars_ = [], []
+        for a in range(0, sample, 2000):
+            Ks = gp_ref.cross_ardse(Xs[a:min(sample, a + 2000)], X, beta, s)
+            means.append(Ks @ alpha)
+            V = sla.solve_triangular(L, Ks.T, lower=True, check_finite=False)
+            vars_.append(s - np.einsum("ij,ij->j", V, V))
+        t_pred = time.perf_counter() - t1
+        runs.append((t_fact + t_pred / sample * m, t_fact, t_pred))
+    runs.sort()
+    t_full, t_fact, t_pred = runs[len(runs) // 2]
     # "reference-faithful": re-factorise per batch of 4 points (assess_all_models.py:481-489)
     t2 = time.perf_counter()
     G4 = gp_ref.gram_ardse(X, beta, s, delta)
@@ -101,10 +131,12 @@ def cpu_baseline(X, y, beta, Xs, s, delta, budget_s: float):
     t4 = time.perf_counter() - t2
     return {
         "value": m / t_full, "unit": "predictions/s", "cores": _CPU_THREADS, "kind": "port",
-        "sample": (f"oracle/gp_ref numpy fp64 (OpenBLAS, {_CPU_THREADS} threads, "
-                   f"{platform.processor() or platform.machine()}): full n={X.shape[0]} "
-                   f"Gram+Cholesky ({t_fact:.2f} s) + predict on the first {done} of {m} test "
-                   f"points ({t_pred:.2f} s), extrapolated linearly to m={m}"),
+        "sample": (f"oracle/gp_ref numpy fp64, OpenBLAS {_CPU_THREADS} threads on "
+                   f"{cpu_model()} (os.cpu_count()={os.cpu_count()}, "
+                   f"affinity={len(os.sched_getaffinity(0))}): full n={X.shape[0]} "
+                   f"Gram+Cholesky + predict of the first {sample} of {m} test points, median of "
+                   f"{reps} runs (fact {t_fact:.2f} s + predict {t_pred:.2f} s), extrapolated "
+                   f"linearly to m={m}"),
         "reference_faithful_value": 4.0 / t4,
         "reference_faithful_sample": ("re-factorise per batch of 4 test points as "
                                       "assess_all_models.py:481-489 does: one batch timed "
@@ -126,20 +158,19 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=4096)
-    ap.add_argument("--m", type=int, default=100000, help="test points per GPU")
+    ap.add_argument("--m", type=int, default=100000, help="test points (whole job)")
     ap.add_argument("--d", type=int, default=8)
     ap.add_argument("--m-chunk", type=int, default=0)
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds for the CPU leg")
+    ap.add_argument("--cpu-sample", type=int, default=20000,
+                    help="test points the CPU baseline predicts per run (median of 3 runs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling leg (N > 1)")
     ap.add_argument("--workload", choices=("c3", "c4", "fit"), default="c3")
     ap.add_argument("--ny", type=int, default=1347945, help="fit: field size per run")
     ap.add_argument("--fit-pcs", type=int, default=8, help="fit: principal components")
     ap.add_argument("--serial", action="store_true",
-                    help="c3: one stream, no overlap at all (gram, potrf, predict in order)")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="c3: alternate two streams so the next step's factorisation runs "
-                         "under the current TRMM (measured no gain: the TRMM holds every CU "
-                         "slot and the factorisation's launches wait behind it)")
+                    help="c3: no context; gram, potrf, cross-covariance, predict in order on "
+                         "one stream")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
     ap.add_argument("--c4-path", choices=("fit_predict", "predict"), default="predict",
                     help="c4: gram -> potrf -> gp_predict (default), or one gp_fit_predict per "
@@ -154,98 +185,113 @@ def main():
     ctx = gdist.init_from_env("cuda")
     dev = ctx.device
     n, m, d = args.n, args.m, args.d
-    X, y, beta, Xs, s, delta = c3_inputs(ctx.rank, n, m, d)
+    X, y, beta, Xs, s, delta = c3_inputs(n, m, d)
+    lo, hi = gdist.shard_range(m, ctx.rank, ctx.world)
+    counts = [gdist.shard_range(m, r, ctx.world)[1] - gdist.shard_range(m, r, ctx.world)[0]
+              for r in range(ctx.world)]
+    ml = hi - lo
     Xd = torch.as_tensor(X, device=dev)
-    Xsd = torch.as_tensor(Xs, device=dev)
+    Xsd = torch.as_tensor(Xs[lo:hi], device=dev).contiguous()
     yd = torch.as_tensor(y, device=dev).reshape(1, n)
     bd = torch.as_tensor(beta, device=dev).reshape(1, d)
     sd = torch.tensor([s], dtype=torch.float64, device=dev)
     dd = torch.tensor([delta], dtype=torch.float64, device=dev)
-    # Default: one gp_fit_predict per step on the current stream (its cross-covariance runs
-    # on a library stream while the factorisation runs).  --pipeline alternates two streams
-    # and two buffer sets so step t+1's Gram + factorisation + cross-covariance run under step
-    # t's TRMM; every step still does all of its own work inside the timed region.
-    nslot = 2 if (args.pipeline and not args.serial) else 1
-    streams = ([torch.cuda.current_stream(dev)] if nslot == 1 else
-               [torch.cuda.Stream(device=dev) for _ in range(nslot)])
-    wss = [kernels.PredictWorkspace() for _ in range(nslot)]
-    outs = [(torch.empty((1, m), dtype=torch.float64, device=dev),
-             torch.empty((1, m), dtype=torch.float64, device=dev)) for _ in range(nslot)]
-    mean, var = outs[0]
-    counter = [0]
+    fctx = None if args.serial else kernels.FitPredictContext(dev)
+    ws = kernels.PredictWorkspace()
+    out = torch.empty((2, ml), dtype=torch.float64, device=dev)   # rows: mean, var
 
-    def step():
-        sl = counter[0] % nslot
-        counter[0] += 1
-        if args.serial:
-            G = kernels.gram(Xd, bd, sd, dd)
-            ch = kernels.cholesky_inverse(G)
-            kernels.predict(ch, Xd, Xsd, bd, sd, sd, yd, m_chunk=args.m_chunk,
-                            workspace=wss[sl], out=outs[sl])
-            return ch
-        with torch.cuda.stream(streams[sl]):
-            _, _, ch = kernels.fit_predict(Xd, Xsd, bd, sd, dd, sd, yd, m_chunk=args.m_chunk,
-                                           workspace=wss[sl], out=outs[sl])
+    def step(Xs_t=Xsd, o=out):
+        return kernels.fit_predict(Xd, Xs_t, bd, sd, dd, sd, yd, m_chunk=args.m_chunk,
+                                   workspace=ws, out=(o[0:1], o[1:2]), ctx=fctx, check=False)[2]
+
+    def timed(fn, steps):
+        gdist.barrier(ctx)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        gdist.barrier(ctx)
+        return gdist.max_over_ranks(ctx, time.perf_counter() - t0)
+
+    gathered = [None]
+
+    def strong_step():
+        ch = step()
+        gathered[0] = gdist.gather_cols(ctx, out, counts)   # (2, m) on rank 0
         return ch
 
     for _ in range(args.warmup):
-        ch = step()
+        ch = strong_step()
     torch.cuda.synchronize()
     ch.check()
     if os.environ.get("GPFIT_BENCH_NOEVENTS") != "1":
         _capi.call("gp_profile_enable", 64 * (args.steps + 1))
     _capi.call("gp_profile_reset")
-
-    gdist.barrier(ctx)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    gdist.barrier(ctx)
-    elapsed = time.perf_counter() - t0
-    elapsed = gdist.max_over_ranks(ctx, elapsed)
-
+    elapsed = timed(strong_step, args.steps)
     prof = {k: read_prof(v) for k, v in (("trmm", _capi.PROF_TRMM), ("gram", _capi.PROF_GRAM),
                                          ("potrf", _capi.PROF_POTRF),
                                          ("cross", _capi.PROF_CROSS))}
     _capi.call("gp_profile_enable", 0)
 
+    weak = None
+    if ctx.world > 1 and not args.no_weak:
+        # weak scaling: rank r predicts its own 100k points (rows [r m, (r+1) m) of rng(2)'s
+        # stream), no collective inside a step
+        Xw = np.random.default_rng(2).random(((ctx.rank + 1) * m, d))[ctx.rank * m:]
+        Xwd = torch.as_tensor(Xw, device=dev).contiguous()
+        ow = torch.empty((2, m), dtype=torch.float64, device=dev)
+        for _ in range(args.warmup):
+            step(Xwd, ow)
+        t_w = timed(lambda: step(Xwd, ow), args.steps)
+        weak = {"value": ctx.world * m * args.steps / t_w, "unit": "predictions/s",
+                "ms_per_step": t_w / args.steps * 1e3, "m_test_per_gpu": m,
+                "note": "every rank predicts its own 100k points (redundant factorisation, "
+                        "no collective)"}
+        del Xwd, ow
+
+    res = gathered[0]
+    if fctx is not None:
+        fctx.close()
     if ctx.rank != 0:
         return
     K = args.steps
-    value = ctx.world * m * K / elapsed
+    value = m * K / elapsed
     # algorithmic work: trmm n^2 + mean/var 4n flop per prediction
     tr_cnt, tr_ms = prof["trmm"]
-    tr_flops = float(m) * K * (n * n + 4 * n)
+    tr_flops = float(ml) * K * (n * n + 4 * n)
     tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic, traffic_src = None, None
-    tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    tj = json.load(open(tf)) if os.path.exists(tf) else {}
     chunk = args.m_chunk or 16384   # the library's default test-point chunk for one GP
-    if tj and n == 4096 and chunk == tj.get("m_chunk"):
-        kt = tj["kernels"].get("trmm_pair_kernel") or tj["kernels"]["trmm_reduce_kernel"]
-        traffic = kt["bytes_per_launch"]
-        traffic_src = "profiles/r01/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+    for rnd in ("r02", "r01"):
+        tf = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        tj = json.load(open(tf)) if os.path.exists(tf) else {}
+        if tj and n == 4096 and chunk == tj.get("m_chunk") and ml == tj.get("m", 100000):
+            traffic = tj["kernels"]["trmm_pair_kernel"]["bytes_per_launch"]
+            traffic_src = (f"profiles/{rnd}/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, per "
+                           "launch)")
+            break
     roof = {"kernel": "trmm_pair_kernel", "bound": "mfma", "achieved": round(tr_tfs, 3),
             "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": traffic_src, "launches": tr_cnt,
             "avg_launch_ms": round(tr_ms / max(tr_cnt, 1), 4),
             "flop_per_launch": tr_flops / max(tr_cnt, 1),
-            "work_note": "n^2 + 4n flop per prediction (lower-triangular L^-1 K*^T + mean/var)"}
+            "work_note": "n^2 + 4n flop per prediction (lower-triangular L^-1 K*^T + mean/var), "
+                         "rank 0's test points"}
     g_cnt, g_ms = prof["gram"]
     g_bytes = (4.0 * n * (n + 1) + 8.0 * n * d) * g_cnt   # lower triangle written + X read
     p_cnt, p_ms = prof["potrf"]
     p_flops = 2.0 * n ** 3 / 3.0 * p_cnt
     c_cnt, c_ms = prof["cross"]
     npad = kernels.padded_n(n)
-    c_bytes = 8.0 * npad * m * K
+    c_bytes = 8.0 * npad * ml * K
     aux = {
         "gram": {"bound": "hbm", "achieved": round(g_bytes / (g_ms * 1e-3) / 1e9, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(g_bytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                 "avg_launch_ms": round(g_ms / max(g_cnt, 1), 4)},
+                 "avg_launch_ms": round(g_ms / max(g_cnt, 1), 4),
+                 "work_note": "4n(n+1) B written (lower triangle) + 8nd B read per launch"},
         "potrf_inv": {"bound": "mfma", "achieved": round(p_flops / (p_ms * 1e-3) / 1e12, 3),
                       "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                       "frac": round(p_flops / (p_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
@@ -254,29 +300,32 @@ def main():
         "cross": {"bound": "hbm", "achieved": round(c_bytes / (c_ms * 1e-3) / 1e9, 1),
                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": round(c_bytes / (c_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                  "ms_per_step": round(c_ms / K, 4)},
+                  "ms_per_step": round(c_ms / K, 4),
+                  "work_note": "8 B written per (padded train row, test point)"},
         "trmm_ms_per_step": round(tr_ms / K, 4),
     }
     line = {
         "metric": METRIC, "value": value, "unit": "predictions/s", "n_gpus": ctx.world,
         "steps": K, "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (SURVEY §8d C3 recipe: seeded uniform design, sin target)",
         "config": {"workload": "C3 single-output ARD-SE GP: Gram + Cholesky/L^-1 + predict",
-                   "n_train": n, "m_test_per_gpu": m, "d": d,
-                   "parallelism": f"test-point shards x{ctx.world}, redundant factorisation",
-                   "pipeline": ("serial" if args.serial else
-                                "gp_fit_predict (cross-covariance overlapped with the "
-                                "factorisation)" if nslot == 1 else
-                                "gp_fit_predict, 2 alternating streams (next factorisation "
-                                "under the current TRMM)")},
-        "roofline": roof, "roofline_aux": aux, "cpu_baseline": None,
+                   "n_train": n, "m_test": m, "d": d, "m_test_rank0": ml,
+                   "parallelism": (f"strong: m/{ctx.world} test-point blocks per rank, "
+                                   "redundant factorisation, (mean, var) gathered to rank 0 "
+                                   "every step" if ctx.world > 1 else "1 GPU"),
+                   "pipeline": ("serial (one stream)" if args.serial else
+                                "gp_fit_predict on a gp_ctx (cross-covariance on a CU-masked "
+                                "stream beside the factorisation)")},
+        "roofline": roof, "roofline_aux": aux, "weak": weak, "cpu_baseline": None,
     }
+    if res is None or tuple(res.shape) != (2, m):
+        raise RuntimeError(f"gathered result has shape {None if res is None else res.shape}")
     if ctx.world == 1 and not args.no_cpu:
-        cb, mu_ref, var_ref = cpu_baseline(X, y, beta, Xs, s, delta, args.cpu_budget)
+        cb, mu_ref, var_ref = cpu_baseline(X, y, beta, Xs, s, delta, args.cpu_sample)
         k = mu_ref.shape[0]
-        mu_g = mean[0, :k].cpu().numpy()
-        var_g = var[0, :k].cpu().numpy()
+        mu_g = res[0, :k].cpu().numpy()
+        var_g = res[1, :k].cpu().numpy()
         cb["parity_vs_gpu"] = {"points": int(k),
                                "max_abs_dmean": float(np.max(np.abs(mu_g - mu_ref))),
                                "max_abs_dvar": float(np.max(np.abs(var_g - var_ref)))}
@@ -308,13 +357,14 @@ def main_c4(args):
     ws = kernels.PredictWorkspace()
     mean = torch.empty((bl, m), dtype=torch.float64, device=dev)
     var = torch.empty((bl, m), dtype=torch.float64, device=dev)
+    fctx = kernels.FitPredictContext(dev) if args.c4_path == "fit_predict" else None
 
     def step():
         if bl and args.c4_path == "fit_predict":
             # one gp_fit_predict over this rank's PCs: the cross-covariance of every chunk runs
-            # on a library stream under the batched factorisation
+            # on the context's stream under the batched factorisation
             kernels.fit_predict(Xd, Xsd, Bl, Sl, Dl, Sl, Wl, m_chunk=args.m_chunk, workspace=ws,
-                                out=(mean, var))
+                                out=(mean, var), ctx=fctx, check=False)
         elif bl:
             G = kernels.gram(Xd, Bl, Sl, Dl, batch=bl)
             ch = kernels.cholesky_inverse(G)
@@ -338,6 +388,8 @@ def main_c4(args):
     tr_cnt, tr_ms = read_prof(_capi.PROF_TRMM)
     p_cnt, p_ms = read_prof(_capi.PROF_POTRF)
     _capi.call("gp_profile_enable", 0)
+    if fctx is not None:
+        fctx.close()
     if ctx.rank != 0:
         return
     K = args.steps

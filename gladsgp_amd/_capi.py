@@ -10,7 +10,6 @@ our kernels share one runtime and one device context.
 """
 from __future__ import annotations
 
-import atexit
 import ctypes
 import os
 
@@ -34,7 +33,15 @@ SIGNATURES = {
                                c_void_p]),
     "gp_potrf_inv": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_ll, c_int,
                              c_void_p, c_void_p, c_void_p]),
+    "gp_potrf": (c_int, [c_void_p, c_int, c_int, c_ll, c_int, c_void_p, c_void_p, c_void_p]),
+    "gp_trtri": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_ll, c_int, c_void_p,
+                         c_void_p]),
     "gp_predict_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
+    "gp_predict_chol_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
+    "gp_predict_chol": (c_int, [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_int, c_int,
+                                c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                c_ll, c_int, c_void_p]),
     "gp_predict": (c_int, [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_int, c_int,
                            c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int, c_void_p]),
@@ -53,8 +60,9 @@ SIGNATURES = {
                                c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int,
-                               c_void_p]),
-    "gp_fit_predict_release": (c_int, []),
+                               c_void_p, c_void_p]),
+    "gp_ctx_create": (c_int, [ctypes.c_double, c_int, c_void_p]),
+    "gp_ctx_destroy": (c_int, [c_void_p]),
     "gp_loglik_ws_bytes": (c_ll, [c_int, c_int]),
     "gp_loglik": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                           c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,
@@ -118,7 +126,7 @@ def lib() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -m gladsgp_amd._build` "
             "(or __graft_entry__.build()); there is no CPU fallback")
     try:
-        handle = ctypes.CDLL(os.environ.get("GPFIT_LIB_AB", LIB_PATH))   # A/B builds
+        handle = ctypes.CDLL(LIB_PATH)
     except OSError as exc:  # pragma: no cover - environment specific
         raise GPFitUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
     for name, (res, args) in SIGNATURES.items():
@@ -126,14 +134,7 @@ def lib() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _LIB = handle
-    atexit.register(_release)    # runs before torch's own exit hooks (registered earlier)
     return handle
-
-
-def _release() -> None:
-    """Drop gp_fit_predict's library streams while the HIP runtime is still alive."""
-    if _LIB is not None and torch.cuda.is_initialized():
-        _LIB.gp_fit_predict_release()
 
 
 def call(name: str, *args) -> int:

@@ -17,6 +17,14 @@
 //
 // diag_factor_inv: barrier-free symmetric elimination in one wave's registers (L), with a
 // second wave applying the same row operations to I (L^-1); see the function.
+//
+// The kernels are templated on MODE, three C-ABI entry points over one sweep:
+//   kPotrfInv (gp_potrf_inv): all of the above;
+//   kPotrf    (gp_potrf)    : the L part only (no X_kc panels, no R tiles); D_k goes to a
+//                             stream-ordered NB x n scratch (LAPACK dpotrf('L') contract);
+//   kTrtri    (gp_trtri)    : the X part only, from a given L: every D_k = L_kk^-1 up front
+//                             (trtri_diag_kernel, all blocks in parallel), then per step k the
+//                             X_kc panels and R tiles (LAPACK dtrtri('L','N') + padding).
 #include "gpfit_common.h"
 #include <cstdlib>
 #include "gpfit_profile.h"
@@ -28,6 +36,14 @@ namespace {
 
 constexpr int NB = 64;
 constexpr int LP = NB + 1;  // LDS pitch (doubles)
+constexpr int kPotrfInv = 0, kPotrf = 1, kTrtri = 2;
+
+// D_k = L_kk^-1: X_kk inside L^-1 (kPotrfInv, kTrtri) or block k of the NB x n scratch
+// (kPotrf, ldx = NB).
+template <int MODE>
+GP_DEV double* dk_ptr(double* Xb, int ldx, int k0) {
+  return Xb + (MODE == kPotrf ? 0 : k0) + (long long)k0 * ldx;
+}
 #ifndef DIAG_PE
 #define DIAG_PE 4           // diag factor: steps between step-counter publications
 #endif
@@ -292,7 +308,8 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
 }
 
 // Factor diagonal block k whose (updated, symmetric) tile is in sm.As as [row][col]; write
-// L_kk into A, D_k into X, accumulate logdet, set info.
+// L_kk into A, D_k into X (dk_ptr), accumulate logdet, set info.
+template <int MODE>
 GP_DEV void diag_block(Smem& sm, double* __restrict__ Ab, int lda, double* __restrict__ Xb,
                        int ldx, int n, int k, int* info, double* logdet, int b) {
   const int k0 = k * NB, nb = min(NB, n - k0);
@@ -304,7 +321,7 @@ GP_DEV void diag_block(Smem& sm, double* __restrict__ Ab, int lda, double* __res
   }
   if (threadIdx.x == 0 && logdet) logdet[b] += lg;
   double* Akk = Ab + k0 + (long long)k0 * lda;
-  double* Xkk = Xb + k0 + (long long)k0 * ldx;
+  double* Xkk = dk_ptr<MODE>(Xb, ldx, k0);
 #pragma unroll 4
   for (int q = 0; q < 16; ++q) {
     int row, col;
@@ -316,6 +333,7 @@ GP_DEV void diag_block(Smem& sm, double* __restrict__ Ab, int lda, double* __res
   }
 }
 
+template <int MODE>
 __global__ __launch_bounds__(256, 2) void chol_diag_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
     long long sX, int n, int k, int* __restrict__ info, double* __restrict__ logdet) {
@@ -337,9 +355,59 @@ __global__ __launch_bounds__(256, 2) void chol_diag_kernel(
     sm.As[row * LP + col] = v;
   }
   __syncthreads();
-  diag_block(sm, Ab, lda, X + b * sX, ldx, n, k, info, logdet, b);
+  diag_block<MODE>(sm, Ab, lda, X + b * sX, ldx, n, k, info, logdet, b);
 }
 
+// kTrtri: D_k = L_kk^-1 for every diagonal block at once (grid N x batch, one wave each).
+// Lane c owns column c of D_k and runs the column-oriented forward substitution
+//   x_j <- x_j / L_jj ;  x_r -= L_rj x_j (r > j)
+// with column j of L_kk read as 16-byte LDS broadcasts (bcast_axpy).  info[b] = first exactly
+// zero (or non-finite) diagonal entry, 1-based (LAPACK dtrtri).
+__global__ __launch_bounds__(64) void trtri_diag_kernel(
+    const double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
+    long long sX, int n, int* __restrict__ info) {
+  LdsSmem& sm = *(LdsSmem*)&g_sm;
+  const int k = blockIdx.x, b = blockIdx.y;
+  const int k0 = k * NB, nb = min(NB, n - k0);
+  const int lane = threadIdx.x;
+  const double* Akk = A + b * sA + k0 + (long long)k0 * lda;
+  lds_double* Lc = sm.As;        // Lc[j * NB + r] = L[r][j], identity padding past nb
+#pragma unroll 4
+  for (int j = 0; j < NB; ++j) {
+    double v;
+    if (j < nb && lane < nb) v = (lane >= j) ? Akk[lane + (long long)j * lda] : 0.0;
+    else v = (lane == j) ? 1.0 : 0.0;
+    Lc[j * NB + lane] = v;
+  }
+  __syncthreads();
+  const double dj = Lc[lane * NB + lane];
+  const bool bad = lane < nb && !(dj != 0.0 && isfinite(dj));
+  const unsigned long long badm = __ballot(bad);
+  if (badm) {
+    if (lane == 0 && info) atomicMin(&info[b], k0 + __ffsll((long long)badm));
+    return;
+  }
+  sm.invs[lane] = 1.0 / dj;
+  __syncthreads();
+  double x[NB];
+#pragma unroll
+  for (int r = 0; r < NB; ++r) x[r] = (r == lane) ? 1.0 : 0.0;
+  static_for<0, NB, 1>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    x[j] *= sm.invs[j];
+    if constexpr (j + 1 < NB) bcast_axpy<j + 1>(x, &Lc[j * NB], x[j]);
+  });
+  // transpose through LDS (Bs[c][r]) so the global stores run down columns
+  lds_double* T = sm.Bs;
+#pragma unroll
+  for (int r = 0; r < NB; ++r) T[lane * LP + r] = x[r];
+  __syncthreads();
+  double* Xkk = X + b * sX + k0 + (long long)k0 * ldx;
+  if (lane < nb)
+    for (int c = 0; c < nb; ++c) Xkk[lane + (long long)c * ldx] = T[c * LP + lane];
+}
+
+template <int MODE>
 __global__ __launch_bounds__(256) void chol_panel_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
     long long sX, int n, int k, int nbelow, const int* __restrict__ info) {
@@ -349,12 +417,12 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
   const int k0 = k * NB, kv = min(NB, n - k0);
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
-  const double* Dk = Xb + k0 + (long long)k0 * ldx;   // D_k = X_kk (lower, zero upper)
+  const double* Dk = dk_ptr<MODE>(Xb, ldx, k0);      // D_k (lower, zero upper)
   // both tile kinds through one code path (a short kernel's cost is largely the code a cold
   // instruction cache streams, see upd_load):
   //   L_ik = A_ik D_k^T : opA = A_ik (NAT, rv rows), opB[p][c] = D_k(c,p) (NAT), C = A_ik
   //   X_kc = D_k R_kc   : opA = D_k (NAT),          opB[p][c] = R_kc(p,c) (TRN), C = R_kc
-  const bool lt = (int)blockIdx.x < nbelow;
+  const bool lt = MODE == kTrtri ? false : (MODE == kPotrf ? true : (int)blockIdx.x < nbelow);
   const double *pa, *pb;
   double* pc;
   int la, av, rv, cv;
@@ -368,7 +436,7 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(
     av = rv;
     pb = Dk;
   } else {
-    const int c0 = (blockIdx.x - nbelow) * NB;
+    const int c0 = ((int)blockIdx.x - (MODE == kTrtri ? 0 : nbelow)) * NB;
     rv = kv;
     cv = NB;
     pc = Xb + k0 + (long long)c0 * ldx;
@@ -510,15 +578,12 @@ GP_DEV void upd_store(const UpdTile& t, const double (&cpre)[16], const double* 
   }
 }
 
-// Trailing update of step k.  Block 0 owns tile (k+1, k+1) and then factors it (lookahead).
-// Blocks 1.. walk the other tiles with stride gridDim.x - 1 (the host caps the grid at two
-// resident blocks per CU), loading the next tile's operands and C into registers while the
-// current tile's MFMAs run.
-// MODE (timing probe, tools/probe_update.hip): 0 = production, 1 = block 0 skips its factor,
-// 2 = block 0 only, 6 = workers return at once, 8 = as 1 with each worker's start / end
-// s_memrealtime written to logdet[2 idx], logdet[2 idx + 1], 9 = as 8 but the workers walk
-// their tiles twice and the stamps bracket the second pass (warm instruction cache).
-template <int MODE = 0>
+// Trailing update of step k.  kPotrfInv / kPotrf: block 0 owns tile (k+1, k+1) and then
+// factors it (lookahead), blocks 1.. walk the other tiles with stride gridDim.x - 1; kTrtri
+// (no A tiles, D_k precomputed): every block walks the R tiles with stride gridDim.x.  The host
+// caps the grid at two resident blocks per CU; each worker loads the next tile's operands and C
+// into registers while the current tile's MFMAs run.
+template <int MODE>
 __global__ __launch_bounds__(256, 2) void chol_update_kernel(
     double* __restrict__ A, int lda, long long sA, double* __restrict__ X, int ldx,
     long long sX, int n, int k, int T, int* __restrict__ info, double* __restrict__ logdet) {
@@ -528,50 +593,43 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(
   const int k0 = k * NB, kv = min(NB, n - k0);
   double* Ab = A + b * sA;
   double* Xb = X + b * sX;
-  const int nt = T * (T + 1) / 2 + T * (k + 1);
-  const int idx = blockIdx.x;
-  const unsigned long long t_start = MODE >= 8 ? __builtin_amdgcn_s_memrealtime() : 0;
-  if ((MODE == 2 || MODE == 6) && idx != 0) return;
-  if (idx != 0) {
+  const int ntri = T * (T + 1) / 2;
+  // tile index space of upd_tile: [0, ntri) A tiles, [ntri, ntri + T(k+1)) R tiles
+  const int t_lo = MODE == kTrtri ? ntri : 0;
+  const int t_hi = ntri + (MODE == kPotrf ? 0 : T * (k + 1));
+  const bool look = MODE != kTrtri;
+  if (!look || blockIdx.x != 0) {
     // one call site each for the loads, the MFMAs, the epilogue and the LDS stores (compact
     // code), software-pipelined: tile i's loads are issued before tile i - stride's MFMAs
-    const int stride = gridDim.x - 1;
-    unsigned long long t_pass = t_start;
-    for (int pass = 0; pass < (MODE == 9 ? 2 : 1); ++pass) {
-      if (MODE == 9) t_pass = __builtin_amdgcn_s_memrealtime();
-      OpTile ta, tb;
-      double cpre[16], cnext[16];
-      UpdTile cur, prev;
-      bool started = false;
-      for (int i = idx;; i += stride) {
-        const bool have = i < nt;                       // uniform
-        if (have) {
-          cur = upd_tile(Ab, lda, Xb, ldx, n, k, T, i);
-          upd_load(cur, lda, kv, ta, tb, cnext);
-        }
-        if (started) {
-          f64x4 acc[2][2];
-          mma64(sm.As, sm.Bs, acc);
-          __syncthreads();
-          acc_to_lds(sm.As, acc);                       // As[col][row] = product
-          __syncthreads();
-          upd_store(prev, cpre, sm.As);
-        }
-        if (!have) break;
-        __syncthreads();                                // the epilogue has read As
-        store_op<false>(sm.As, ta);
-        if (cur.trn) store_op<true>(sm.Bs, tb);
-        else store_op<false>(sm.Bs, tb);
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 16; ++q) cpre[q] = cnext[q];
-        prev = cur;
-        started = true;
+    const int stride = look ? gridDim.x - 1 : gridDim.x;
+    OpTile ta, tb;
+    double cpre[16], cnext[16];
+    UpdTile cur, prev;
+    bool started = false;
+    for (int i = t_lo + blockIdx.x;; i += stride) {
+      const bool have = i < t_hi;                     // uniform
+      if (have) {
+        cur = upd_tile(Ab, lda, Xb, ldx, n, k, T, i);
+        upd_load(cur, lda, kv, ta, tb, cnext);
       }
-    }
-    if ((MODE == 8 || MODE == 9) && threadIdx.x == 0) {
-      logdet[2 * idx] = (double)t_pass;
-      logdet[2 * idx + 1] = (double)__builtin_amdgcn_s_memrealtime();
+      if (started) {
+        f64x4 acc[2][2];
+        mma64(sm.As, sm.Bs, acc);
+        __syncthreads();
+        acc_to_lds(sm.As, acc);                       // As[col][row] = product
+        __syncthreads();
+        upd_store(prev, cpre, sm.As);
+      }
+      if (!have) break;
+      __syncthreads();                                // the epilogue has read As
+      store_op<false>(sm.As, ta);
+      if (cur.trn) store_op<true>(sm.Bs, tb);
+      else store_op<false>(sm.Bs, tb);
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) cpre[q] = cnext[q];
+      prev = cur;
+      started = true;
     }
     return;
   }
@@ -591,43 +649,45 @@ __global__ __launch_bounds__(256, 2) void chol_update_kernel(
   __syncthreads();
   acc_to_lds(sm.As, acc);      // As[col][row] = product
   __syncthreads();
-  {
-    // tile (k+1, k+1): updated lower values -> symmetric [row][col] tile in As, then factor
+  // tile (k+1, k+1): updated lower values -> symmetric [row][col] tile in As, then factor
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      int row, col;
-      slot_rc(q, row, col);
-      cpre[q] -= sm.As[col * LP + row];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      int row, col;
-      slot_rc(q, row, col);
-      if (row < rv && col < cv) {
-        if (row >= col) {
-          sm.As[row * LP + col] = cpre[q];
-          sm.As[col * LP + row] = cpre[q];
-        }
-      } else {
-        sm.As[row * LP + col] = (row == col) ? 1.0 : 0.0;
-      }
-    }
-    __syncthreads();
-    if (MODE == 0 || MODE == 2) diag_block(sm, Ab, lda, Xb, ldx, n, k + 1, info, logdet, b);
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    cpre[q] -= sm.As[col * LP + row];
   }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    if (row < rv && col < cv) {
+      if (row >= col) {
+        sm.As[row * LP + col] = cpre[q];
+        sm.As[col * LP + row] = cpre[q];
+      }
+    } else {
+      sm.As[row * LP + col] = (row == col) ? 1.0 : 0.0;
+    }
+  }
+  __syncthreads();
+  diag_block<MODE>(sm, Ab, lda, Xb, ldx, n, k + 1, info, logdet, b);
+}
+
+// info sentinel (memset 0x7f) -> 0 for problems whose diagonal was fine (gp_trtri).
+__global__ void trtri_info_kernel(int* __restrict__ info, int batch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < batch && info[b] == 0x7f7f7f7f) info[b] = 0;
 }
 
 }  // namespace
 
 static_assert(GPFIT_POTRF_NB == NB, "gpfit_internal.h must match the blocking");
 
-// Grid of chol_update_kernel for nt tiles per problem: block 0 plus workers, capped at two
-// resident blocks per CU over the whole batch so every worker is resident and walks several
-// tiles (GPFIT_UPD_CAP overrides the cap; 0 = one block per tile).
+// Grid of chol_update_kernel for nt tiles per problem, capped at two resident blocks per CU
+// over the whole batch so every worker is resident and walks several tiles.
 static int update_grid(int nt, int batch) {
   static const int cap_all = [] {
-    if (const char* e = getenv("GPFIT_UPD_CAP")) return atoi(e);
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -635,10 +695,57 @@ static int update_grid(int nt, int batch) {
       ncu = 256;
     return 2 * ncu;
   }();
-  if (cap_all <= 0) return nt;
   int cap = cap_all / (batch > 0 ? batch : 1);
   if (cap < 2) cap = 2;
   return nt < cap ? nt : cap;
+}
+
+#define GP_CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return GPFIT_ERR_HIP - (int)e_; } while (0)
+
+// The blocked sweep shared by the three entry points (arguments already validated; X is L^-1
+// (kPotrfInv, kTrtri, zero-filled by the caller) or the D_k scratch (kPotrf)).
+template <int MODE>
+static int potrf_sweep(double* A, int n, int lda, long long sA, double* X, int ldx, long long sX,
+                       int batch, int* info, double* logdet, hipStream_t stream, int k_ev,
+                       hipEvent_t ev) {
+  const int N = gp_ceil_div(n, NB);
+  if (MODE != kTrtri) {   // kTrtri: every D_k is made up front by trtri_diag_kernel
+    hipLaunchKernelGGL(chol_diag_kernel<MODE>, dim3(batch), dim3(256), 0, stream, A, lda, sA, X,
+                       ldx, sX, n, 0, info, logdet);
+    GP_CK(hipGetLastError());
+  }
+  for (int k = 0; k < N; ++k) {
+    const int T = N - k - 1;
+    const int npanel = MODE == kPotrfInv ? T + k : (MODE == kPotrf ? T : k);
+    if (npanel > 0) {
+      hipLaunchKernelGGL(chol_panel_kernel<MODE>, dim3(npanel, batch), dim3(256), 0, stream, A,
+                         lda, sA, X, ldx, sX, n, k, T, info);
+      GP_CK(hipGetLastError());
+    }
+    if (T > 0) {
+      const int nt = (MODE == kTrtri ? 0 : T * (T + 1) / 2) + (MODE == kPotrf ? 0 : T * (k + 1));
+      hipLaunchKernelGGL(chol_update_kernel<MODE>, dim3(update_grid(nt, batch), batch), dim3(256), 0, stream, A,
+                         lda, sA, X, ldx, sX, n, k, T, info, logdet);
+      GP_CK(hipGetLastError());
+    }
+    if (ev && (k == k_ev || (k == N - 1 && k_ev >= N))) GP_CK(hipEventRecord(ev, stream));
+  }
+  return 0;
+}
+
+// Zero L^-1 (upper triangle + padding): one memset for a packed batch, else one 2-D memset per
+// problem.
+static hipError_t zero_linv(double* Linv, int npad, int ldinv, long long strideInv, int batch,
+                            hipStream_t stream) {
+  if (ldinv == npad && (batch == 1 || strideInv == (long long)npad * npad))
+    return hipMemsetAsync(Linv, 0, sizeof(double) * ((long long)(batch - 1) * strideInv +
+                                                     (long long)ldinv * npad), stream);
+  for (int b = 0; b < batch; ++b) {
+    hipError_t e = hipMemset2DAsync(Linv + b * strideInv, sizeof(double) * ldinv, 0,
+                                    sizeof(double) * npad, npad, stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double* Linv,
@@ -661,42 +768,63 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
   if (batch > 1 && strideInv < (long long)ldinv * npad) return -7;
   if (batch < 0) return -8;
   if (n == 0 || batch == 0) return 0;
-  hipError_t e;
-#define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
   if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
-  // zero L^-1 (upper triangle + padding): one memset for a packed batch, else one 2-D memset
-  // per problem
-  if (ldinv == npad && (batch == 1 || strideInv == (long long)npad * npad)) {
-    GP_CK(hipMemsetAsync(Linv, 0, sizeof(double) * ((long long)(batch - 1) * strideInv +
-                                                    (long long)ldinv * npad), stream));
-  } else {
-    for (int b = 0; b < batch; ++b)
-      GP_CK(hipMemset2DAsync(Linv + b * strideInv, sizeof(double) * ldinv, 0,
-                             sizeof(double) * npad, npad, stream));
-  }
-  const int N = gp_ceil_div(n, NB);
+  GP_CK(zero_linv(Linv, npad, ldinv, strideInv, batch, stream));
   gpfit_prof_begin(GP_PROF_POTRF, stream);
-  hipLaunchKernelGGL(chol_diag_kernel, dim3(batch), dim3(256), 0, stream, A, lda, strideA,
-                     Linv, ldinv, strideInv, n, 0, info, logdet);
-  GP_CK(hipGetLastError());
-  for (int k = 0; k < N; ++k) {
-    const int T = N - k - 1;
-    if (T + k > 0) {
-      hipLaunchKernelGGL(chol_panel_kernel, dim3(T + k, batch), dim3(256), 0, stream, A, lda,
-                         strideA, Linv, ldinv, strideInv, n, k, T, info);
-      GP_CK(hipGetLastError());
-    }
-    if (T > 0) {
-      const int nt = T * (T + 1) / 2 + T * (k + 1);
-      hipLaunchKernelGGL(chol_update_kernel<0>, dim3(update_grid(nt, batch), batch), dim3(256), 0,
-                         stream, A, lda,
-                         strideA, Linv, ldinv, strideInv, n, k, T, info, logdet);
-      GP_CK(hipGetLastError());
-    }
-    if (ev && (k == k_ev || (k == N - 1 && k_ev >= N))) GP_CK(hipEventRecord(ev, stream));
-  }
+  const int rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info,
+                                        logdet, stream, k_ev, ev);
   gpfit_prof_end(GP_PROF_POTRF, stream);
-#undef GP_CK
-  return 0;
+  return rc;
 }
+
+extern "C" int gp_potrf(double* A, int n, int lda, long long strideA, int batch, int* info,
+                        double* logdet, hipStream_t stream) {
+  if (!A) return -1;
+  if (n < 0) return -2;
+  if (lda < n || lda < 1) return -3;
+  if (batch > 1 && strideA < (long long)lda * n) return -4;
+  if (batch < 0) return -5;
+  if (n == 0 || batch == 0) return 0;
+  if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
+  if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
+  // D_k scratch: NB x (N NB) per problem, stream-ordered (freed when the sweep has run)
+  const int N = gp_ceil_div(n, NB);
+  const long long sD = (long long)NB * N * NB;
+  double* D = nullptr;
+  GP_CK(hipMallocAsync(reinterpret_cast<void**>(&D), sizeof(double) * sD * batch, stream));
+  const int rc = potrf_sweep<kPotrf>(A, n, lda, strideA, D, NB, sD, batch, info, logdet, stream,
+                                     -1, nullptr);
+  GP_CK(hipFreeAsync(D, stream));
+  return rc;
+}
+
+extern "C" int gp_trtri(const double* L, int n, int ldl, long long strideL, double* Linv,
+                        int ldinv, long long strideInv, int batch, int* info,
+                        hipStream_t stream) {
+  if (!L) return -1;
+  if (n < 0) return -2;
+  if (ldl < n || ldl < 1) return -3;
+  if (batch > 1 && strideL < (long long)ldl * n) return -4;
+  if (!Linv) return -5;
+  const int npad = gp_padded_n(n);
+  if (ldinv < npad || ldinv < 1) return -6;
+  if (batch > 1 && strideInv < (long long)ldinv * npad) return -7;
+  if (batch < 0) return -8;
+  if (n == 0 || batch == 0) return 0;
+  // trtri_diag_kernel lowers info[b] (atomicMin) from a "none" sentinel; the sweep's kernels
+  // then skip every problem with info != 0
+  if (info) GP_CK(hipMemsetAsync(info, 0x7f, sizeof(int) * batch, stream));
+  GP_CK(zero_linv(Linv, npad, ldinv, strideInv, batch, stream));
+  hipLaunchKernelGGL(trtri_diag_kernel, dim3(gp_ceil_div(n, NB), batch), dim3(64), 0, stream,
+                     L, ldl, strideL, Linv, ldinv, strideInv, n, info);
+  GP_CK(hipGetLastError());
+  if (info) {
+    hipLaunchKernelGGL(trtri_info_kernel, dim3(gp_ceil_div(batch, 256)), dim3(256), 0, stream,
+                       info, batch);
+    GP_CK(hipGetLastError());
+  }
+  return potrf_sweep<kTrtri>(const_cast<double*>(L), n, ldl, strideL, Linv, ldinv, strideInv,
+                             batch, info, nullptr, stream, -1, nullptr);
+}
+#undef GP_CK

@@ -22,7 +22,7 @@
 #include "gpfit_profile.h"
 #include "gpfit_internal.h"
 #include "../../include/gpfit.h"
-#include <mutex>
+#include <new>
 #include <vector>
 
 namespace {
@@ -127,122 +127,11 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256, 2) void trmm_reduce_kernel(
-    const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt2,
-    int mc, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
-    int NI, int NC, int order) {
-  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
-  const int b = blockIdx.y;
-  int t = blockIdx.x;
-  int I, C;
-  if (order == 0 || order == 3) {    // row-major: heaviest row tiles of every panel first
-    if (order == 3) t = xcd_remap(t, NI * NC);   // ... consecutive panels of a row on one XCD
-    I = NI - 1 - t / NC;
-    C = t % NC;
-  } else {                           // panel-major: all row tiles of a test-point panel
-    if (order == 2) t = xcd_remap(t, NI * NC);   // ... on one XCD (shares the B panel in L2)
-    C = t / NI;
-    I = NI - 1 - t % NI;
-  }
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
-  const double* L = Linv + b * sL + I * BI + 2 * lane;                 // + k*ld per row
-  const double* K = Kt2 + b * sK + (long long)C * BC + 2 * lane;       // + k*mc per row
-  const int nsteps = (I + 1) * (BI / BK);
-
-  auto issue = [&](int s, double* st) {
-    const int k0 = s * BK;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {              // A rows k0 + 4w + r
-      const int kr = 4 * w + r;
-      glds16(L + (long long)(k0 + kr) * ld, st + kr * APITCH);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {              // B rows k0 + 4w + r
-      const int kr = 4 * w + r;
-      glds16(K + (long long)(k0 + kr) * mc, st + ASTAGE + kr * BC);
-    }
-  };
-
-  f64x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[a][c] = zero4();
-
-  issue(0, smem);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // K steps [0, s_diag) lie left of the tile's diagonal block (every product counts); the
-  // last BI/BK steps cross it, where each wave skips its 16-row MFMA tiles that only meet the
-  // zero upper triangle of L^-1 (3% of the TRMM's MFMAs at n = 4096).
-  // Codegen note: the next-stage issue stays behind a branch the compiler cannot fold
-  // (nsteps laundered through an SGPR), so it remains its own basic block as in a single
-  // loop; with the branch folded away the scheduler moved the barrier and its vmcnt(0) wait
-  // up among the MFMAs and exposed the load latency every step (1.10 vs 1.01 ms per launch).
-  const int s_diag = nsteps - BI / BK;
-  int nst = nsteps;
-  asm volatile("" : "+s"(nst));
-  int s = 0;
-  for (; s < s_diag; ++s) {
-    double* cur = smem + (s & 1) * STAGE;
-    if (s + 1 < nst) issue(s + 1, smem + ((s + 1) & 1) * STAGE);
-    trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  for (; s < nsteps; ++s) {
-    double* cur = smem + (s & 1) * STAGE;
-    if (s + 1 < nst) issue(s + 1, smem + ((s + 1) & 1) * STAGE);
-    const int lo = (s - s_diag) - 4 * wr;   // wave-uniform
-    if (lo < 4) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, lo);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // epilogue: column partial sums of V*z and V^2 over this tile's 128 rows
-  double* red = smem;   // [2 wr][2 kind][BC]; the loop's last barrier retired all LDS reads
-  const double* zb = z + (long long)b * npad + I * BI + wr * 64;
-  double zr[4][4];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) zr[mi][r] = zb[mi * 16 + lk + 4 * r];
-#pragma unroll
-  for (int nj = 0; nj < 4; ++nj) {
-    double sm = 0.0, sv = 0.0;
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double v = acc[mi][nj][r];
-        sm = fma(v, zr[mi][r], sm);
-        sv = fma(v, v, sv);
-      }
-    sm += __shfl_xor(sm, 16, 64);
-    sv += __shfl_xor(sv, 16, 64);
-    sm += __shfl_xor(sm, 32, 64);
-    sv += __shfl_xor(sv, 32, 64);
-    if (lk == 0) {
-      red[(wr * 2 + 0) * BC + wc * 64 + nj * 16 + li] = sm;
-      red[(wr * 2 + 1) * BC + wc * 64 + nj * 16 + li] = sv;
-    }
-  }
-  __syncthreads();
-  if (tid < BC) {
-    const int col = C * BC + tid;
-    double* pm = part + ((long long)(b * 2 + 0) * NI + I) * mc;
-    double* pv = part + ((long long)(b * 2 + 1) * NI + I) * mc;
-    pm[col] = red[0 * BC + tid] + red[2 * BC + tid];
-    pv[col] = red[1 * BC + tid] + red[3 * BC + tid];
-  }
-}
-
 // Row-tile pairs: block (p, C) computes tile (NI-1-p, C) and then tile (p, C), so every block
 // runs 8(NI+1) K steps (uniform work: at C3 the 512 blocks of a chunk are exactly one
 // residency wave of 2 per CU, no tail) and the second tile's first stage is fetched under the
-// first tile's last MFMAs.  Loop bodies as in trmm_reduce_kernel.
+// first tile's last MFMAs.  Per K step: the next stage's global_load_lds is issued, then the
+// MFMAs of the current stage, then one vmcnt(0) + barrier.
 __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
     const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt2,
     int mc, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
@@ -393,29 +282,6 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
                                batch, st);
 }
 
-// Tile order of trmm_reduce: 0 row-major (tiles sharing an L^-1 row panel run together),
-// 1 panel-major, 2 panel-major + XCD remap, 3 row-major + XCD remap.  Measured on MI355X
-// (tools/sweep_trmm.sh, profiles/r01): row-major wins (66 TF/s at C3 vs 36-58 for the
-// panel-major orders).  GPFIT_TRMM_ORDER overrides the default for experiments.
-int trmm_order() {
-  static int v = [] {
-    const char* e = getenv("GPFIT_TRMM_ORDER");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// Row-tile pairs per block (trmm_pair_kernel, the default) or one tile per block in the
-// GPFIT_TRMM_ORDER dispatch order (GPFIT_TRMM_PAIR=0).  Same-box A/B: C4 (n = 1024) 2.226 ->
-// 2.122 ms per launch, C3 1.002-1.008 -> 1.001-1.003 (profiles/r01/ab_trmm_pair.log).
-bool trmm_pair() {
-  static const int v = [] {
-    const char* e = getenv("GPFIT_TRMM_PAIR");
-    return e ? atoi(e) : 1;
-  }();
-  return v != 0;
-}
-
 struct Plan {
   int npad, NI, mc, NC, nchunks, slabs;
   long long off_z, off_kt, off_part, bytes, slab_elems, part_elems;
@@ -542,14 +408,9 @@ hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, con
   const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
   const int ncol_tiles = gp_ceil_div(mv, BC);
   if (fin) gpfit_prof_begin(GP_PROF_TRMM, stream);
-  if (trmm_pair())
-    hipLaunchKernelGGL(trmm_pair_kernel, dim3((p.NI + 1) / 2 * ncol_tiles, batch), dim3(256), 0,
-                       stream, Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z,
-                       p.npad, part, p.NI, ncol_tiles);
-  else
-    hipLaunchKernelGGL(trmm_reduce_kernel, dim3(p.NI * ncol_tiles, batch), dim3(256), 0, stream,
-                       Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z, p.npad,
-                       part, p.NI, ncol_tiles, trmm_order());
+  hipLaunchKernelGGL(trmm_pair_kernel, dim3((p.NI + 1) / 2 * ncol_tiles, batch), dim3(256), 0,
+                     stream, Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z,
+                     p.npad, part, p.NI, ncol_tiles);
   if (fin) gpfit_prof_end(GP_PROF_TRMM, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !fin) return e;
@@ -658,110 +519,101 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
 }
 
 // ------------------------------------------------------------------------------------------
-// gp_fit_predict: Gram -> Cholesky/L^-1 -> predict as one stream-ordered operation on `stream`,
-// internally forked over three library streams (equal priority):
+// gp_fit_predict: Gram -> Cholesky/L^-1 -> predict as one stream-ordered operation on `stream`.
+// With a context (gp_ctx_create) it forks over the context's three streams (equal priority):
 //   fact: Gram, then the blocked factorisation (latency-bound, few CUs busy);
-//   aux : the cross-covariance of every chunk (independent of the factorisation);
+//   aux : the cross-covariance of every chunk (independent of the factorisation), CU-masked so
+//         that it leaves aux_free_cus CUs to the factorisation, from the factorisation's
+//         block step cross_start * n/64 on;
 //   pred: once both are done, z = L^-1 w, then per chunk the TRMM (all row tiles of the
-//         chunk, so its K* stays cached) and its mean / var.
-// The operation joins back into `stream`.  A caller that alternates two streams (and two
-// buffer sets) between consecutive calls gets the next problem's factorisation and
-// cross-covariance running under the current problem's TRMM: the fact/aux streams only wait
-// for their own call's inputs, not for the previous call's prediction.
-namespace {
-
-struct FitPredictStreams {
+//         chunk, so its K* stays cached) and one mean / var pass over all m points;
+// and joins back into `stream`.  Without a context every step runs in order on `stream`.
+struct gp_ctx_s {
+  int device = -1;
+  double cross_start = 0.4;
   hipStream_t fact = nullptr, aux = nullptr, pred = nullptr;
   hipEvent_t e_start = nullptr, e_fact = nullptr, e_aux = nullptr, e_done = nullptr;
   hipEvent_t e_late = nullptr;   // the factorisation has turned latency-bound
 };
 
-// Block step of the n/64 blocked factorisation from which the HBM-bound cross-covariance runs
-// beside it.  On all CUs, started at once it doubled the early (bandwidth-bound) trailing
-// updates (54 -> 123 us) and 0.6 was best (30.2 / 29.85 / 29.78 / 29.85 / 30.07 ms at 0 / 0.5 /
-// 0.6 / 0.7 / 0.8); on the CU-masked stream (aux_free_cus) 0.25 was best, and 0.4 with 128
-// free CUs once the cross-covariance kernel stopped branching around its exps (it got faster
-// and leaned harder on the factorisation: profiles/r01/ab_cross_select_exp.log).
-// GPFIT_CROSS_START (fraction of the steps, 0 = at once) overrides.
-int late_step(int nblk) {
-  static double f = [] {
-    const char* e = getenv("GPFIT_CROSS_START");
-    return e ? atof(e) : 0.4;
-  }();
-  const int k = (int)(f * nblk);
-  return k < 0 ? 0 : k;
-}
-// CUs the cross-covariance stream leaves free for the factorisation (GPFIT_AUX_FREE_CUS).
-// With CUs reserved the cross-covariance can start early without stretching the
-// factorisation's latency-bound tail: 64 reserved took the C3 step 29.37 -> 29.13 ms with a
-// start at 25% of the block steps (profiles/r01/ab_update_persistent_auxmask*.log); with the
-// faster, branch-free cross-covariance kernel 128 reserved and a start at 40% matched the old
-// kernel's C3 step while C4 (where it runs alone) gained 1.2%.
-int aux_free_cus() {
-  static int v = [] {
-    const char* e = getenv("GPFIT_AUX_FREE_CUS");
-    return e ? atoi(e) : 128;
-  }();
-  return v;
-}
-std::mutex g_fp_mu;
-FitPredictStreams g_fp[64];
+namespace {
 
-hipError_t fit_predict_streams(FitPredictStreams** out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
+// Defaults measured at C3 (profiles/r01): the cross-covariance on all CUs started at once
+// doubled the early, bandwidth-bound trailing updates (54 -> 123 us); on a CU-masked stream
+// that leaves 128 of 256 CUs free, a start at 40% of the block steps was best
+// (profiles/r01/ab_cross_select_exp.log, ab_update_persistent_auxmask*.log).
+constexpr double kCrossStart = 0.4;
+constexpr int kAuxFreeCUs = 128;
+
+hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
+  hipError_t e = hipGetDevice(&c->device);
   if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  std::lock_guard<std::mutex> lk(g_fp_mu);
-  FitPredictStreams& S = g_fp[dev];
-  if (!S.fact) {
-    if ((e = hipStreamCreateWithFlags(&S.fact, hipStreamNonBlocking)) != hipSuccess) return e;
-    if ((e = hipStreamCreateWithFlags(&S.pred, hipStreamNonBlocking)) != hipSuccess) return e;
-    // the cross-covariance stream may leave aux_free_cus() CUs to the factorisation it runs
-    // beside (logical CU i sits on XCD i % 8, tools/probe_cumask.hip: the low CUs are spread
-    // evenly over the XCDs)
-    const int fr = aux_free_cus();
-    int ncu = 0;
-    if (fr > 0 &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        fr < ncu) {
-      std::vector<uint32_t> m((ncu + 31) / 32, 0u);
-      for (int i = fr; i < ncu; ++i) m[i / 32] |= 1u << (i % 32);
-      if ((e = hipExtStreamCreateWithCUMask(&S.aux, (uint32_t)m.size(), m.data())) != hipSuccess)
-        return e;
-    } else if ((e = hipStreamCreateWithFlags(&S.aux, hipStreamNonBlocking)) != hipSuccess) {
+  c->cross_start = cross_start < 0 ? kCrossStart : cross_start;
+  const int fr = aux_free_cus < 0 ? kAuxFreeCUs : aux_free_cus;
+  if ((e = hipStreamCreateWithFlags(&c->fact, hipStreamNonBlocking)) != hipSuccess) return e;
+  if ((e = hipStreamCreateWithFlags(&c->pred, hipStreamNonBlocking)) != hipSuccess) return e;
+  // logical CU i sits on XCD i % 8 (measured with a CU-mask probe in round 1), so masking off
+  // the low CUs reserves CUs evenly per XCD
+  int ncu = 0;
+  if (fr > 0 &&
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) ==
+          hipSuccess &&
+      fr < ncu) {
+    std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+    for (int i = fr; i < ncu; ++i) m[i / 32] |= 1u << (i % 32);
+    if ((e = hipExtStreamCreateWithCUMask(&c->aux, (uint32_t)m.size(), m.data())) != hipSuccess)
       return e;
-    }
-    hipEvent_t* ev[5] = {&S.e_start, &S.e_fact, &S.e_aux, &S.e_done, &S.e_late};
-    for (hipEvent_t* p : ev)
-      if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
+  } else if ((e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess) {
+    return e;
   }
-  *out = &S;
+  hipEvent_t* ev[5] = {&c->e_start, &c->e_fact, &c->e_aux, &c->e_done, &c->e_late};
+  for (hipEvent_t* p : ev)
+    if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
   return hipSuccess;
+}
+
+hipError_t ctx_fini(gp_ctx_s* c) {
+  hipError_t first = hipSuccess;
+  auto keep = [&](hipError_t e) { if (first == hipSuccess && e != hipSuccess) first = e; };
+  int dev0 = 0;
+  keep(hipGetDevice(&dev0));
+  if (c->device >= 0) keep(hipSetDevice(c->device));
+  hipStream_t st[3] = {c->fact, c->aux, c->pred};
+  for (hipStream_t x : st)
+    if (x) {
+      keep(hipStreamSynchronize(x));
+      keep(hipStreamDestroy(x));
+    }
+  hipEvent_t ev[5] = {c->e_start, c->e_fact, c->e_aux, c->e_done, c->e_late};
+  for (hipEvent_t x : ev)
+    if (x) keep(hipEventDestroy(x));
+  if (c->device >= 0) keep(hipSetDevice(dev0));
+  return first;
 }
 
 }  // namespace
 
-extern "C" int gp_fit_predict_release(void) {
-  std::lock_guard<std::mutex> lk(g_fp_mu);
-  int dev0 = 0;
-  hipError_t e = hipGetDevice(&dev0);
-  if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
-  for (int dev = 0; dev < 64; ++dev) {
-    FitPredictStreams& S = g_fp[dev];
-    if (!S.fact) continue;
-    if ((e = hipSetDevice(dev)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
-    hipStream_t st[3] = {S.fact, S.aux, S.pred};
-    for (hipStream_t x : st) {
-      if ((e = hipStreamSynchronize(x)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
-      if ((e = hipStreamDestroy(x)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
-    }
-    hipEvent_t ev[5] = {S.e_start, S.e_fact, S.e_aux, S.e_done, S.e_late};
-    for (hipEvent_t x : ev)
-      if ((e = hipEventDestroy(x)) != hipSuccess) return GPFIT_ERR_HIP - (int)e;
-    S = FitPredictStreams{};
+extern "C" int gp_ctx_create(double cross_start, int aux_free_cus, void** ctx) {
+  if (cross_start > 1.0) return -1;
+  if (!ctx) return -3;
+  *ctx = nullptr;
+  gp_ctx_s* c = new (std::nothrow) gp_ctx_s();
+  if (!c) return GPFIT_ERR_HIP - (int)hipErrorOutOfMemory;
+  const hipError_t e = ctx_init(c, cross_start, aux_free_cus);
+  if (e != hipSuccess) {
+    (void)ctx_fini(c);
+    delete c;
+    return GPFIT_ERR_HIP - (int)e;
   }
-  e = hipSetDevice(dev0);
+  *ctx = c;
+  return 0;
+}
+
+extern "C" int gp_ctx_destroy(void* ctx) {
+  if (!ctx) return 0;
+  gp_ctx_s* c = static_cast<gp_ctx_s*>(ctx);
+  const hipError_t e = ctx_fini(c);
+  delete c;
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }
 
@@ -771,7 +623,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
                               int ldw, double* G, int ldg, long long strideG, double* Linv,
                               int ldinv, long long strideInv, int* info, double* logdet,
                               double* mean, double* var, int ldo, int batch, void* ws,
-                              long long ws_bytes, int m_chunk, hipStream_t stream) {
+                              long long ws_bytes, int m_chunk, void* ctx, hipStream_t stream) {
   int rc = check_common(X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch);
   if (rc) return rc;
   rc = check_solve(Linv, ldinv, strideInv, n, s_pred, w_hat, ldw, m, mean, var, ldo, batch);
@@ -785,40 +637,87 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   if (!ws) return -21;
   if (ws_bytes < p.bytes) return -22;
   const WS w = carve(p, ws);
-  FitPredictStreams* S = nullptr;
+  gp_ctx_s* S = static_cast<gp_ctx_s*>(ctx);
+  if (S) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != S->device) return -29;
+  }
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
-  GP_CK(fit_predict_streams(&S));
-  GP_CK(hipEventRecord(S->e_start, stream));
-  GP_CK(hipStreamWaitEvent(S->fact, S->e_start, 0));
+  hipStream_t fact = S ? S->fact : stream, aux = S ? S->aux : stream, pred = S ? S->pred : stream;
+  if (S) {
+    GP_CK(hipEventRecord(S->e_start, stream));
+    GP_CK(hipStreamWaitEvent(fact, S->e_start, 0));
+  }
   // fact: Gram -> Cholesky / L^-1, with e_late once the factorisation is latency-bound
-  rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, S->fact);
+  rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, fact);
   if (rc) return rc;
   const int nblk = gp_ceil_div(n, GPFIT_POTRF_NB);
-  const int k_late = late_step(nblk);
-  if (k_late == 0) GP_CK(hipEventRecord(S->e_late, S->fact));
+  const int k_late = S ? (int)(S->cross_start * nblk) : -1;
+  if (S && k_late <= 0) GP_CK(hipEventRecord(S->e_late, fact));
   rc = gpfit_potrf_inv_event(G, n, ldg, strideG, Linv, ldinv, strideInv, batch, info, logdet,
-                             S->fact, k_late > 0 ? k_late : -1, k_late > 0 ? S->e_late : nullptr);
+                             fact, k_late > 0 ? k_late : -1,
+                             (S && k_late > 0) ? S->e_late : nullptr);
   if (rc) return rc;
-  GP_CK(hipEventRecord(S->e_fact, S->fact));
-  // aux: cross-covariance of every chunk, from the factorisation's latency-bound phase on
-  GP_CK(hipStreamWaitEvent(S->aux, S->e_late, 0));
-  gpfit_prof_begin_n(GP_PROF_CROSS, S->aux, p.nchunks);   // one event pair, all chunks
+  if (S) {
+    GP_CK(hipEventRecord(S->e_fact, fact));
+    GP_CK(hipStreamWaitEvent(aux, S->e_late, 0));
+  }
+  // aux: cross-covariance of every chunk (one timing-event pair around all of them)
+  gpfit_prof_begin_n(GP_PROF_CROSS, aux, p.nchunks);
   for (int ch = 0; ch < p.nchunks; ++ch)
     GP_CK(cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n, m, d,
-                      beta, ldbeta, s, batch, S->aux));
-  gpfit_prof_end(GP_PROF_CROSS, S->aux);
-  GP_CK(hipEventRecord(S->e_aux, S->aux));
+                      beta, ldbeta, s, batch, aux));
+  gpfit_prof_end(GP_PROF_CROSS, aux);
   // pred: z, then TRMM + mean / var chunk by chunk.  One launch per chunk (not one for all):
   // the dispatcher interleaves another stream's kernels between launches, so a concurrent
   // factorisation is not starved behind a 25 ms grid (measured: 14 ms vs 3 ms per potrf).
-  GP_CK(hipStreamWaitEvent(S->pred, S->e_fact, 0));
-  GP_CK(hipStreamWaitEvent(S->pred, S->e_aux, 0));
+  if (S) {
+    GP_CK(hipEventRecord(S->e_aux, aux));
+    GP_CK(hipStreamWaitEvent(pred, S->e_fact, 0));
+    GP_CK(hipStreamWaitEvent(pred, S->e_aux, 0));
+  }
   GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
-                          S->pred));
-  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, S->pred));
-  GP_CK(hipEventRecord(S->e_done, S->pred));
-  GP_CK(hipStreamWaitEvent(stream, S->e_done, 0));
+                          pred));
+  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, pred));
+  if (S) {
+    GP_CK(hipEventRecord(S->e_done, pred));
+    GP_CK(hipStreamWaitEvent(stream, S->e_done, 0));
+  }
 #undef GP_CK
   return 0;
+}
+
+// gp_predict from a Cholesky factor L (LAPACK layout): L^-1 by gp_trtri into the head of the
+// workspace, then gp_predict with the rest.
+extern "C" long long gp_predict_chol_ws_bytes(int n, int m, int batch, int m_chunk) {
+  if (n <= 0 || m <= 0 || batch <= 0) return 0;
+  const long long npad = gp_padded_n(n);
+  return ((8LL * npad * npad * batch + 255) / 256) * 256 + make_plan(n, m, batch, m_chunk).bytes;
+}
+
+extern "C" int gp_predict_chol(const double* L, int ldl, long long strideL, const double* X,
+                               int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                               const double* beta, int ldbeta, const double* s,
+                               const double* s_pred, const double* w_hat, int ldw, double* mean,
+                               double* var, int ldo, int batch, int* info, void* ws,
+                               long long ws_bytes, int m_chunk, hipStream_t stream) {
+  if (!L) return -1;
+  if (ldl < n || ldl < 1) return -2;
+  if (batch > 1 && strideL < (long long)ldl * n) return -3;
+  int rc = check_common(X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch);
+  if (rc) return rc;
+  if (n == 0 || m == 0 || batch == 0) return 0;
+  if (m_chunk < 0) return -24;
+  if (!ws) return -22;
+  if (ws_bytes < gp_predict_chol_ws_bytes(n, m, batch, m_chunk)) return -23;
+  const long long npad = gp_padded_n(n);
+  const long long head = ((8LL * npad * npad * batch + 255) / 256) * 256;
+  double* Linv = static_cast<double*>(ws);
+  rc = gp_trtri(L, n, ldl, strideL, Linv, (int)npad, npad * npad, batch, info, stream);
+  if (rc) return rc;
+  rc = gp_predict(Linv, (int)npad, npad * npad, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s,
+                  s_pred, w_hat, ldw, mean, var, ldo, batch, static_cast<char*>(ws) + head,
+                  ws_bytes - head, m_chunk, stream);
+  return rc;
 }

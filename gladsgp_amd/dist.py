@@ -4,8 +4,11 @@ The GP emulator shards without a data-path exchange:
   * multivariate emulator (C4/C5): the P x S independent (sample, PC) GPs are dealt
     round-robin to ranks; inputs are broadcast once from rank 0, per-rank (mean, var) blocks are
     gathered to rank 0 once at the end;
-  * single-output GP (C2/C3): every rank factorises the same n x n Gram redundantly (~1 ms at
-    n = 4096) and predicts its own block of test points.
+  * single-output GP (C2/C3): every rank factorises the same n x n Gram redundantly (~3 ms at
+    n = 4096) and predicts its contiguous block of the test points; the (mean, var) blocks are
+    gathered to rank 0 (``gather_cols``);
+  * field reconstruction (get_y): the basis K is split by output columns, the PC weights are
+    all-gathered (``all_gather_rows``) and every rank reconstructs its column block.
 
 The reference has no distributed code at all (SLURM job arrays of the external
 simulator only), so there is no call pattern to mirror; collectives here are the minimum the
@@ -33,31 +36,38 @@ class Context:
         return self.backend is not None
 
 
-def init_from_env(device_type: str | None = None) -> Context:
-    """Join the process group described by RANK/WORLD_SIZE/MASTER_* (torchrun), if any."""
+def init_from_env(device_type: str | None = None, backend: str | None = None,
+                  device_index: int | None = None) -> Context:
+    """Join the process group described by RANK/WORLD_SIZE/MASTER_* (torchrun), if any.
+
+    Defaults: one GPU per rank (cuda:LOCAL_RANK) over RCCL.  ``backend="gloo"`` with
+    ``device_index`` lets several ranks share one GPU (the multi-rank GPU tests on a 1-GPU box;
+    collectives then stage through the host)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        idx = local_rank if device_index is None else device_index
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
-    backend = None
     if world > 1:
-        backend = "nccl" if device_type == "cuda" else "gloo"
+        backend = backend or ("nccl" if device_type == "cuda" else "gloo")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            kw = {"device_id": device} if device_type == "cuda" else {}
+            kw = {"device_id": device} if backend == "nccl" else {}
             dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    else:
+        backend = None
     return Context(rank, world, local_rank, device, backend)
 
 
 def barrier(ctx: Context) -> None:
     if ctx.distributed:
-        if ctx.device.type == "cuda":
+        if ctx.device.type == "cuda" and ctx.backend == "nccl":
             dist.barrier(device_ids=[ctx.local_rank])
         else:
             dist.barrier()
@@ -66,7 +76,7 @@ def barrier(ctx: Context) -> None:
 def max_over_ranks(ctx: Context, value: float) -> float:
     if not ctx.distributed:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=ctx.device)
+    t = _wire(ctx, torch.tensor([value], dtype=torch.float64, device=ctx.device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -74,7 +84,10 @@ def max_over_ranks(ctx: Context, value: float) -> float:
 def broadcast_(ctx: Context, t: torch.Tensor, src: int = 0) -> torch.Tensor:
     """In-place broadcast of ``t`` from ``src`` (RCCL over xGMI on the GPU path)."""
     if ctx.distributed:
-        dist.broadcast(t, src=src)
+        w = _wire(ctx, t)
+        dist.broadcast(w, src=src)
+        if w is not t:
+            t.copy_(w)
     return t
 
 
@@ -90,6 +103,12 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return a, a + q + (1 if rank < r else 0)
 
 
+def _wire(ctx: Context, t: torch.Tensor) -> torch.Tensor:
+    """Tensor as the backend moves it: gloo (the CPU test backend, also used to run two ranks
+    on one GPU) only carries host tensors; RCCL carries device tensors in place."""
+    return t.cpu() if (ctx.backend == "gloo" and t.is_cuda) else t
+
+
 def gather_rows(ctx: Context, local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:
     """Gather variable-length row blocks (dim 0) to rank 0; returns the concatenation there.
 
@@ -103,11 +122,48 @@ def gather_rows(ctx: Context, local: torch.Tensor, counts: list[int]) -> torch.T
     pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     if local.shape[0]:
         pad[: local.shape[0]] = local
+    pad = _wire(ctx, pad)
     bufs = [torch.empty_like(pad) for _ in range(ctx.world)] if ctx.rank == 0 else None
     dist.gather(pad, gather_list=bufs, dst=0)
     if ctx.rank != 0:
         return None
-    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0).to(local.device)
+
+
+def gather_cols(ctx: Context, local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:
+    """Gather variable-length column blocks (last dim) to rank 0, concatenated in rank order.
+
+    The strong-scaled single-output GP: rank r holds (mean, var) of its contiguous
+    test-point block ``shard_range(m, r, N)`` as a (2, m_r) tensor; rank 0 receives (2, m).
+    One padded equal-shape ``gather`` (RCCL / gloo); other ranks get None.
+    """
+    if not ctx.distributed:
+        return local
+    mx = max(counts)
+    lead = tuple(local.shape[:-1])
+    pad = torch.zeros(lead + (mx,), dtype=local.dtype, device=local.device)
+    pad[..., : local.shape[-1]] = local
+    pad = _wire(ctx, pad)
+    bufs = [torch.empty_like(pad) for _ in range(ctx.world)] if ctx.rank == 0 else None
+    dist.gather(pad, gather_list=bufs, dst=0)
+    if ctx.rank != 0:
+        return None
+    return torch.cat([b[..., :c] for b, c in zip(bufs, counts)], dim=-1).to(local.device)
+
+
+def all_gather_rows(ctx: Context, local: torch.Tensor, counts: list[int]) -> torch.Tensor:
+    """Every rank receives the rank-order concatenation of variable-length row blocks (dim 0)
+    — the all-gather of the PC weights w before the sharded field reconstruction (§8e)."""
+    if not ctx.distributed:
+        return local
+    mx = max(counts)
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if local.shape[0]:
+        pad[: local.shape[0]] = local
+    pad = _wire(ctx, pad)
+    bufs = [torch.empty_like(pad) for _ in range(ctx.world)]
+    dist.all_gather(bufs, pad)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0).to(local.device)
 
 
 class NativeComm:

@@ -297,21 +297,50 @@ def predict_solve(chol: Cholesky, prep: Prepared, s_pred, w,
     return mean, var
 
 
-_SIDE: dict = {}
+class FitPredictContext:
+    """Caller-owned execution context of :func:`fit_predict` (``gp_ctx_create``): the three
+    library streams (factorisation | CU-masked cross-covariance | prediction) on ``device``.
 
+    Destroy it with :meth:`close` (or use it as a context manager) while the HIP runtime is up:
+    the owner decides the teardown order, the library keeps no global state.
+    """
 
-def side_stream(device) -> torch.cuda.Stream:
-    key = str(device)
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=device)
-    return _SIDE[key]
+    def __init__(self, device=None, cross_start: float = -1.0, aux_free_cus: int = -1):
+        import ctypes
+        self.device = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+        self._h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _capi.call("gp_ctx_create", float(cross_start), int(aux_free_cus),
+                       ctypes.addressof(self._h))
+
+    @property
+    def handle(self) -> int | None:
+        return self._h.value
+
+    def close(self) -> None:
+        if self._h.value:
+            with torch.cuda.device(self.device):
+                _capi.call("gp_ctx_destroy", self._h.value)
+            self._h.value = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def fit_predict(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
-                workspace: PredictWorkspace | None = None, out=None):
-    """Gram -> Cholesky/L^-1 -> predict for ``batch`` GPs in one gp_fit_predict call: the
-    cross-covariance runs on a library stream under the factorisation's latency-bound tail,
-    then the per-chunk TRMM + mean/var.  Returns (mean, var, chol)."""
+                workspace: PredictWorkspace | None = None, out=None,
+                ctx: FitPredictContext | None = None, check: bool = True):
+    """Gram -> Cholesky/L^-1 -> predict for ``batch`` GPs in one gp_fit_predict call.
+
+    With ``ctx`` the cross-covariance runs on the context's CU-masked stream under the
+    factorisation's latency-bound tail, then the per-chunk TRMM + mean/var; without it every
+    step runs in order on the current stream.  ``check`` synchronises and raises if a Gram was
+    not positive definite (its mean / var would be unspecified).  Returns (mean, var, chol).
+    """
     dev = X.device
     X = _as_f64(X, dev, "X")
     Xs = _as_f64(Xs, dev, "Xs")
@@ -336,32 +365,83 @@ def fit_predict(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
         mean, var = out
     nbytes = _capi.lib().gp_fit_predict_ws_bytes(n, m, batch, int(m_chunk))
     ws = (workspace or PredictWorkspace()).get(nbytes, dev)
+    if ctx is not None and ctx.device != dev:
+        raise ValueError(f"context is on {ctx.device}, inputs on {dev}")
     _capi.call("gp_fit_predict", X.data_ptr(), d, Xs.data_ptr(), d, n, m, d, beta_t.data_ptr(),
                d, s_t.data_ptr(), d_t.data_ptr(), sp_t.data_ptr(), w_t.data_ptr(), n,
                G.data_ptr(), n, n * n, Linv.data_ptr(), npad, npad * npad, info.data_ptr(),
                logdet.data_ptr(), mean.data_ptr(), var.data_ptr(),
                mean.stride(0) if batch > 1 else m, batch, ws.data_ptr(), ws.numel(),
-               int(m_chunk), _stream(dev))
-    return mean, var, Cholesky(n, G, Linv, info, logdet)
-
-
-def fit_predict_streams(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
-                        workspace: PredictWorkspace | None = None, out=None):
-    """Previous scheme (kept for comparison): cross-covariance on a torch side stream during
-    the factorisation, then the whole TRMM after it.  Returns (mean, var, chol)."""
-    dev = X.device
-    bt = torch.as_tensor(beta)
-    batch = bt.shape[0] if bt.dim() == 2 else 1
-    main = torch.cuda.current_stream(dev)
-    side = side_stream(dev)
-    ws = workspace or PredictWorkspace()
-    n, m = X.shape[0], Xs.shape[0]
-    ws.get(_capi.lib().gp_predict_prepared_ws_bytes(n, m, batch, int(m_chunk)), dev)
-    side.wait_stream(main)                       # inputs and workspace are ready
-    with torch.cuda.stream(side):
-        prep = predict_prepare(X, Xs, beta, s, batch, m_chunk, ws)
-    G = gram(X, beta, s, delta, batch=batch)
-    ch = cholesky_inverse(G)
-    main.wait_stream(side)
-    mean, var = predict_solve(ch, prep, s_pred, w, out=out)
+               int(m_chunk), ctx.handle if ctx is not None else None, _stream(dev))
+    ch = Cholesky(n, G, Linv, info, logdet)
+    if check:
+        ch.check()
     return mean, var, ch
+
+
+def cholesky(G: torch.Tensor, overwrite: bool = True):
+    """Plain blocked Cholesky (gp_potrf, LAPACK dpotrf('L')): returns (L, info, logdet) with L
+    the lower factor as a (batch, n, n) logical tensor."""
+    _check_device(G, "G")
+    if G.dtype != F64:
+        raise TypeError("G must be float64")
+    if G.dim() == 2:
+        G = G.unsqueeze(0)
+    batch, n, n2 = G.shape
+    if n != n2:
+        raise ValueError("G must be square")
+    A = G if (overwrite and G.is_contiguous()) else G.contiguous().clone()
+    info = torch.empty(batch, dtype=torch.int32, device=G.device)
+    logdet = torch.empty(batch, dtype=F64, device=G.device)
+    _capi.call("gp_potrf", A.data_ptr(), n, n, n * n, batch, info.data_ptr(), logdet.data_ptr(),
+               _stream(G.device))
+    return torch.tril(A.transpose(-1, -2)), info, logdet
+
+
+def _lapack_buf(L: torch.Tensor) -> torch.Tensor:
+    """(batch, n, n) logical lower factor -> contiguous column-major buffer [b, j, i] = L[i, j]."""
+    _check_device(L, "L")
+    if L.dim() == 2:
+        L = L.unsqueeze(0)
+    return L.to(F64).transpose(-1, -2).contiguous()
+
+
+def trtri(L: torch.Tensor) -> Cholesky:
+    """L^-1 of a lower factor (gp_trtri, LAPACK dtrtri('L','N')); returns a :class:`Cholesky`
+    whose ``info`` flags a zero diagonal, usable with :func:`predict` / :func:`nll`."""
+    Lb = _lapack_buf(L)
+    batch, n, _ = Lb.shape
+    npad = padded_n(n)
+    Linv = torch.empty((batch, npad, npad), dtype=F64, device=Lb.device)
+    info = torch.empty(batch, dtype=torch.int32, device=Lb.device)
+    _capi.call("gp_trtri", Lb.data_ptr(), n, n, n * n, Linv.data_ptr(), npad, npad * npad, batch,
+               info.data_ptr(), _stream(Lb.device))
+    logdet = 2.0 * torch.log(torch.diagonal(Lb, dim1=-2, dim2=-1)).sum(-1)
+    return Cholesky(n, Lb, Linv, info, logdet)
+
+
+def predict_chol(L: torch.Tensor, X, Xs, beta, s, s_pred, w, m_chunk: int = 0,
+                 workspace: PredictWorkspace | None = None):
+    """Posterior mean / variance from a Cholesky factor L (gp_predict_chol: gp_trtri into the
+    workspace, then gp_predict).  Returns (mean, var, info)."""
+    Lb = _lapack_buf(L)
+    dev = Lb.device
+    batch, n, _ = Lb.shape
+    X = _as_f64(X, dev, "X")
+    Xs = _as_f64(Xs, dev, "Xs")
+    d = X.shape[1]
+    m = Xs.shape[0]
+    beta_t = _beta(beta, batch, d, dev)
+    s_t = _per_batch(s, batch, dev, "s")
+    sp_t = _per_batch(s_pred, batch, dev, "s_pred")
+    w_t = _as_f64(w, dev, "w").reshape(batch, n)
+    mean = torch.empty((batch, m), dtype=F64, device=dev)
+    var = torch.empty((batch, m), dtype=F64, device=dev)
+    info = torch.empty(batch, dtype=torch.int32, device=dev)
+    nbytes = _capi.lib().gp_predict_chol_ws_bytes(n, m, batch, int(m_chunk))
+    ws = (workspace or PredictWorkspace()).get(nbytes, dev)
+    _capi.call("gp_predict_chol", Lb.data_ptr(), n, n * n, X.data_ptr(), d, Xs.data_ptr(), d, n,
+               m, d, beta_t.data_ptr(), d, s_t.data_ptr(), sp_t.data_ptr(), w_t.data_ptr(), n,
+               mean.data_ptr(), var.data_ptr(), m, batch, info.data_ptr(), ws.data_ptr(),
+               ws.numel(), int(m_chunk), _stream(dev))
+    return mean, var, info

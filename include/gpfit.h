@@ -8,8 +8,10 @@
  * Python-side binding is gladsgp_amd/_capi.py (ctypes) and is shown in INTEGRATION.md.
  *
  * Conventions (all entry points):
- *  - every pointer is caller-owned DEVICE memory (the library never allocates; the predict
- *    workspace is sized by gp_predict_ws_bytes() and passed in);
+ *  - every pointer is caller-owned DEVICE memory.  The library allocates nothing persistent:
+ *    workspaces are sized by the *_ws_bytes() functions and passed in; the only library-owned
+ *    objects are the streams/events of an explicit gp_ctx (gp_ctx_create / gp_ctx_destroy),
+ *    and gp_potrf's stream-ordered D_k scratch (hipMallocAsync / hipFreeAsync in the call);
  *  - matrices are column-major with a leading dimension (LAPACK layout), element (i,j) at
  *    A[i + j*ld]; design matrices X (n x d) are row-major with row stride ldx >= d;
  *  - `batch` independent problems share X / Xs; per-problem operands advance by the given
@@ -80,6 +82,27 @@ int gp_potrf_inv(double* A, int n, int lda, long long strideA,
                  double* Linv, int ldinv, long long strideInv,
                  int batch, int* info, double* logdet, hipStream_t stream);
 
+/*
+ * Plain blocked Cholesky, LAPACK dpotrf('L') per problem: A_b = L_b L_b^T with L_b in the lower
+ * triangle of A_b (strict upper triangle untouched), logdet[b] = log|A_b|, info[b] = 0 or the
+ * 1-based order of the first non-positive-definite leading minor.  Same sweep and arithmetic as
+ * gp_potrf_inv without the inverse (L is bit-identical to gp_potrf_inv's).  info / logdet may
+ * be NULL.  Replaces the factorisation SURVEY §8b names gp_potrf (LAPACK potrf inside SEPIA's
+ * likelihood, scipy.linalg.cholesky in examples/01...ipynb:66,144).
+ */
+int gp_potrf(double* A, int n, int lda, long long strideA, int batch, int* info,
+             double* logdet, hipStream_t stream);
+
+/*
+ * Triangular inverse of a lower Cholesky factor, LAPACK dtrtri('L','N') into a padded buffer:
+ * Linv_b = L_b^-1 (lower; upper triangle and padding to gp_padded_n(n) zeroed), so a caller
+ * that already holds a LAPACK factor can call gp_predict without re-factorising.  info[b] =
+ * 0, or the 1-based index of the first zero (or non-finite) diagonal entry (then Linv_b is
+ * unspecified).  info may be NULL.
+ */
+int gp_trtri(const double* L, int n, int ldl, long long strideL, double* Linv, int ldinv,
+             long long strideInv, int batch, int* info, hipStream_t stream);
+
 /* Bytes of device workspace gp_predict needs for (n, m, batch) with test-point chunk m_chunk
  * (0 = library default).  Workspace contents are scratch (no state between calls).         */
 long long gp_predict_ws_bytes(int n, int m, int batch, int m_chunk);
@@ -99,6 +122,20 @@ int gp_predict(const double* Linv, int ldinv, long long strideInv,
                const double* beta, int ldbeta, const double* s, const double* s_pred,
                const double* w_hat, int ldw, double* mean, double* var, int ldo,
                int batch, void* ws, long long ws_bytes, int m_chunk, hipStream_t stream);
+
+/*
+ * gp_predict from the Cholesky factor L itself (the §8b form, LAPACK layout, lower): L^-1 by
+ * gp_trtri into the head of `ws`, then gp_predict.  `ws` holds
+ * gp_predict_chol_ws_bytes(n, m, batch, m_chunk) bytes; info as gp_trtri (mean / var of a
+ * problem with info[b] != 0 are unspecified).
+ */
+long long gp_predict_chol_ws_bytes(int n, int m, int batch, int m_chunk);
+int gp_predict_chol(const double* L, int ldl, long long strideL,
+                    const double* X, int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                    const double* beta, int ldbeta, const double* s, const double* s_pred,
+                    const double* w_hat, int ldw, double* mean, double* var, int ldo,
+                    int batch, int* info, void* ws, long long ws_bytes, int m_chunk,
+                    hipStream_t stream);
 
 /*
  * Two-phase form of gp_predict.  The cross-covariance of every test-point chunk does not depend
@@ -136,15 +173,28 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
            int batch, hipStream_t stream);
 
 /*
+ * Execution context of gp_fit_predict, created and destroyed by the caller on the current
+ * device: three streams (factorisation | cross-covariance | prediction) and their events.
+ *   cross_start  : fraction of the factorisation's n/64 block steps after which the
+ *                  cross-covariance starts (< 0: default 0.4; 0 = at once);
+ *   aux_free_cus : CUs the cross-covariance stream leaves to the factorisation (CU mask;
+ *                  < 0: default 128; 0 = no mask).
+ * gp_ctx_destroy drains the streams and frees them; call it before the HIP runtime is torn
+ * down (e.g. before process exit).  A context serves one host thread at a time.
+ */
+int gp_ctx_create(double cross_start, int aux_free_cus, void** ctx);
+int gp_ctx_destroy(void* ctx);
+
+/*
  * Fit + predict in one call:
  *   G = gram(X) (caller buffer, L on return) -> L, L^-1, info, logdet (as gp_potrf_inv) ->
  *   mean / var at the m test points (as gp_predict).
- * Forks from `stream` into three library-owned streams (Gram + factorisation | cross-
- * covariance of every chunk | then per chunk the TRMM + mean/var) and joins
- * back; the caller sees one stream-ordered operation.  Callers that alternate two streams and
- * two buffer sets between consecutive calls overlap the next factorisation with the current
- * TRMM.  `ws` holds gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes.  Not re-entrant
- * across host threads on the same device (the internal streams are shared).
+ * With ctx == NULL every step runs in order on `stream`.  With a context it forks from
+ * `stream` into the context's streams (Gram + factorisation | cross-covariance of every chunk,
+ * CU-masked, from the factorisation's latency-bound phase on | then per chunk the TRMM and one
+ * mean/var pass) and joins back: the caller sees one stream-ordered operation.  `ws` holds
+ * gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes.  The prediction runs whatever info
+ * says: mean / var of a problem with info[b] != 0 are unspecified (check info).
  * Replaces the reference's fit-then-predict sequence per GP (SEPIA likelihood factorisation +
  * SepiaEmulatorPrediction, time_predictions.py:76-79) at the bench configuration.
  */
@@ -154,15 +204,7 @@ int gp_fit_predict(const double* X, int ldx, const double* Xs, int ldxs, int n, 
                    const double* s_pred, const double* w_hat, int ldw, double* G, int ldg,
                    long long strideG, double* Linv, int ldinv, long long strideInv, int* info,
                    double* logdet, double* mean, double* var, int ldo, int batch, void* ws,
-                   long long ws_bytes, int m_chunk, hipStream_t stream);
-
-/*
- * Drain and destroy gp_fit_predict's library streams (on every device that has them); the
- * next gp_fit_predict re-creates them.  The Python binding calls it at interpreter exit, while
- * the HIP runtime is still up: the cross-covariance stream is CU-masked, and a masked queue
- * left to the runtime's own teardown crashed the process exit under rocprofv3.
- */
-int gp_fit_predict_release(void);
+                   long long ws_bytes, int m_chunk, void* ctx, hipStream_t stream);
 
 /*
  * Batched GP log-likelihood in one stream-ordered call: Gram (gp_gram_ardse) -> Cholesky

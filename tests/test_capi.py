@@ -98,7 +98,7 @@ def test_argument_validation_returns_lapack_style_codes(lib):
                                                                                        1, 0)
     args = [dummy, 2, dummy, 2, 100, 10, 2, dummy, 2, dummy, dummy, dummy, dummy, 100,
             dummy, 100, 10000, dummy, 128, 128 * 128, None, None, dummy, dummy, 10, 1, dummy,
-            1 << 40, 0, None]
+            1 << 40, 0, None, None]
     bad = list(args)
     bad[10] = None                                   # delta
     assert lib.gp_fit_predict(*bad) == -24
@@ -108,6 +108,31 @@ def test_argument_validation_returns_lapack_style_codes(lib):
     bad = list(args)
     bad[27] = 16                                     # workspace too small
     assert lib.gp_fit_predict(*bad) == -22
+
+
+def test_new_entry_points_validate(lib):
+    """gp_potrf / gp_trtri / gp_predict_chol / gp_ctx_*: argument checks before any launch."""
+    dummy = ctypes.c_void_p(16)
+    assert lib.gp_potrf(None, 4, 4, 16, 1, None, None, None) == -1
+    assert lib.gp_potrf(dummy, 4, 3, 16, 1, None, None, None) == -3
+    assert lib.gp_potrf(dummy, 4, 4, 8, 2, None, None, None) == -4
+    assert lib.gp_potrf(dummy, 0, 1, 0, 1, None, None, None) == 0
+    assert lib.gp_trtri(None, 4, 4, 16, dummy, 128, 128 * 128, 1, None, None) == -1
+    assert lib.gp_trtri(dummy, 4, 4, 16, dummy, 64, 128 * 128, 1, None, None) == -6
+    assert lib.gp_trtri(dummy, 4, 4, 16, None, 128, 128 * 128, 1, None, None) == -5
+    assert lib.gp_predict_chol_ws_bytes(4096, 100000, 1, 0) == (
+        8 * 4096 * 4096 + lib.gp_predict_ws_bytes(4096, 100000, 1, 0))
+    args = [dummy, 100, 10000, dummy, 2, dummy, 2, 100, 10, 2, dummy, 2, dummy, dummy, dummy,
+            100, dummy, dummy, 10, 1, None, dummy, 1 << 40, 0, None]
+    bad = list(args)
+    bad[0] = None
+    assert lib.gp_predict_chol(*bad) == -1
+    bad = list(args)
+    bad[22] = 16                                     # workspace too small
+    assert lib.gp_predict_chol(*bad) == -23
+    assert lib.gp_ctx_create(2.0, 0, dummy) == -1
+    assert lib.gp_ctx_create(0.4, 0, None) == -3
+    assert lib.gp_ctx_destroy(None) == 0
 
 
 def test_comm_argument_validation(lib):

@@ -262,7 +262,8 @@ def test_cpu_tensor_rejected(dev):
 
 
 def test_two_phase_predict_and_overlap_match_single(dev):
-    """gp_predict_cross + gp_predict_solve (and the side-stream fit_predict) == gp_predict."""
+    """gp_predict_cross + gp_predict_solve and gp_fit_predict (serial and with a context)
+    == gp_predict, bit for bit."""
     from gladsgp_amd import kernels
     rng = np.random.default_rng(21)
     n, m, d, B = 333, 5000, 8, 3
@@ -278,15 +279,17 @@ def test_two_phase_predict_and_overlap_match_single(dev):
     prep = kernels.predict_prepare(Xd, Xsd, _t(betas, dev), _t(s, dev), batch=B, m_chunk=1024)
     m2, v2 = kernels.predict_solve(ch, prep, _t(s, dev), _t(W, dev))
     assert torch.equal(m1, m2) and torch.equal(v1, v2)
-    # gp_fit_predict: the TRMM of finished L^-1 row tiles overlapped with the factorisation
-    m3, v3, ch3 = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
-                                      _t(s, dev), _t(W, dev), m_chunk=1024)
-    torch.cuda.synchronize()
+    # gp_fit_predict with a context: cross-covariance on the masked stream under the
+    # factorisation; and without one: every step in order on the caller's stream
+    with kernels.FitPredictContext(dev) as fctx:
+        m3, v3, ch3 = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                          _t(s, dev), _t(W, dev), m_chunk=1024, ctx=fctx)
+        torch.cuda.synchronize()
     assert torch.equal(m1, m3) and torch.equal(v1, v3)
     assert torch.equal(ch3.L, ch.L) and torch.equal(ch3.Linv, ch.Linv)
     assert torch.equal(ch3.logdet, ch.logdet) and int(ch3.info.abs().sum()) == 0
-    m4, v4, _ = kernels.fit_predict_streams(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
-                                            _t(s, dev), _t(W, dev), m_chunk=1024)
+    m4, v4, _ = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                    _t(s, dev), _t(W, dev), m_chunk=1024)
     torch.cuda.synchronize()
     assert torch.equal(m1, m4) and torch.equal(v1, v4)
 
@@ -306,9 +309,10 @@ def test_fit_predict_edge_shapes(dev, n, m, B):
     Xd, Xsd = _t(X, dev), _t(Xs, dev)
     ch = kernels.cholesky_inverse(kernels.gram(Xd, _t(betas, dev), _t(s, dev), _t(delta, dev)))
     m1, v1 = kernels.predict(ch, Xd, Xsd, _t(betas, dev), _t(s, dev), _t(s, dev), _t(W, dev))
-    m2, v2, ch2 = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
-                                      _t(s, dev), _t(W, dev))
-    torch.cuda.synchronize()
+    with kernels.FitPredictContext(dev) as fctx:
+        m2, v2, ch2 = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                          _t(s, dev), _t(W, dev), ctx=fctx)
+        torch.cuda.synchronize()
     assert torch.equal(m1, m2) and torch.equal(v1, v2)
     assert torch.equal(ch.logdet, ch2.logdet)
     for b in range(B):
@@ -327,8 +331,11 @@ def test_fit_predict_reports_non_pd(dev):
     s = np.array([1.0, 1.0])
     delta = np.array([1e-4, -3.0])          # problem 1 is indefinite
     W = rng.standard_normal((2, n))
+    with pytest.raises(ValueError, match="not positive definite"):   # check=True (default)
+        kernels.fit_predict(_t(X, dev), _t(Xs, dev), _t(betas, dev), _t(s, dev),
+                            _t(delta, dev), _t(s, dev), _t(W, dev))
     mean, var, ch = kernels.fit_predict(_t(X, dev), _t(Xs, dev), _t(betas, dev), _t(s, dev),
-                                        _t(delta, dev), _t(s, dev), _t(W, dev))
+                                        _t(delta, dev), _t(s, dev), _t(W, dev), check=False)
     torch.cuda.synchronize()
     info = ch.info.cpu().numpy()
     assert info[0] == 0 and info[1] > 0
@@ -353,3 +360,103 @@ def test_native_comm_world1(dev):
     assert torch.equal(x, torch.arange(1000, dtype=torch.float64, device=dev))
     assert g.shape == (1, 1000) and torch.equal(g[0], x)
     comm.close()
+
+
+@pytest.mark.parametrize("n,B", [(1, 1), (63, 2), (64, 1), (200, 3), (777, 2), (1500, 1)])
+def test_potrf_plain_matches_potrf_inv(dev, n, B):
+    """gp_potrf (L only, LAPACK dpotrf('L')) == gp_potrf_inv's L bit for bit, with the same
+    logdet; the strict upper triangle is left untouched."""
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(n)
+    X = rng.random((n, 6))
+    betas = rng.uniform(0.5, 4, (B, 6))
+    s = rng.uniform(0.5, 2, B)
+    delta = rng.uniform(1e-6, 1e-3, B)
+    G = kernels.gram(_t(X, dev), _t(betas, dev), _t(s, dev), _t(delta, dev))
+    G2 = G.clone()
+    ch = kernels.cholesky_inverse(G)
+    sentinel = torch.triu(torch.full_like(G2, 7.0), diagonal=1).transpose(-1, -2)
+    G2 = torch.where(sentinel == 7.0, sentinel, G2).contiguous()   # buffer's strict upper = 7
+    L, info, logdet = kernels.cholesky(G2)
+    torch.cuda.synchronize()
+    assert int(info.abs().sum()) == 0
+    assert torch.equal(L, ch.L)
+    assert torch.equal(logdet, ch.logdet)
+    assert bool((torch.triu(G2.transpose(-1, -2), diagonal=1)[
+        torch.triu(torch.ones(n, n, device=dev, dtype=torch.bool), diagonal=1).expand(B, n, n)]
+        == 7.0).all())
+    for b in range(B):
+        ref = np.linalg.cholesky(gp_ref.gram_ardse(X, betas[b], s[b], delta[b]))
+        np.testing.assert_allclose(L[b].cpu().numpy(), ref, rtol=0, atol=1e-12)
+
+
+def test_potrf_plain_reports_non_pd(dev):
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(5)
+    X = rng.random((300, 3))
+    G = kernels.gram(_t(X, dev), _t(np.ones((2, 3)), dev), _t([1.0, 1.0], dev),
+                     _t([1e-4, -3.0], dev))
+    ref_info = gp_ref.cholesky(gp_ref.gram_ardse(X, np.ones(3), 1.0, -3.0))[1]
+    _, info, _ = kernels.cholesky(G)
+    info = info.cpu().numpy()
+    assert info[0] == 0 and info[1] == ref_info
+
+
+@pytest.mark.parametrize("n,B", [(1, 1), (64, 1), (65, 2), (300, 3), (1100, 1)])
+def test_trtri_matches_inverse(dev, n, B):
+    """gp_trtri(L) vs numpy's inverse of the same L, and vs gp_potrf_inv's L^-1."""
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(n + 1)
+    X = rng.random((n, 5))
+    betas = rng.uniform(0.5, 3, (B, 5))
+    G = kernels.gram(_t(X, dev), _t(betas, dev), _t(np.ones(B), dev), _t(np.full(B, 1e-3), dev))
+    ch = kernels.cholesky_inverse(G)
+    tr = kernels.trtri(ch.L)
+    torch.cuda.synchronize()
+    assert int(tr.info.abs().sum()) == 0
+    npad = kernels.padded_n(n)
+    Li = tr.linv_buf.transpose(-1, -2).cpu().numpy()
+    assert np.all(Li[:, :n, n:] == 0) and np.all(Li[:, n:, :] == 0)
+    for b in range(B):
+        L = ch.L[b].cpu().numpy()
+        inv = np.linalg.inv(L)
+        X_ = Li[b, :n, :n]
+        assert np.all(np.triu(X_, 1) == 0)
+        scale = np.abs(inv).max()
+        assert np.max(np.abs(X_ - inv)) <= 1e-10 * scale
+        assert np.max(np.abs(X_ @ L - np.eye(n))) <= 1e-10
+        assert np.max(np.abs(X_ - ch.Linv[b].cpu().numpy())) <= 1e-10 * scale
+    assert npad == Li.shape[-1]
+    # log|A| from the factor agrees with the factorisation's
+    np.testing.assert_allclose(tr.logdet.cpu().numpy(), ch.logdet.cpu().numpy(), rtol=1e-12)
+
+
+def test_trtri_reports_zero_diagonal(dev):
+    from gladsgp_amd import kernels
+    L = torch.eye(130, dtype=torch.float64, device=dev).repeat(2, 1, 1)
+    L[1, 70, 70] = 0.0
+    tr = kernels.trtri(L)
+    assert tr.info.cpu().tolist() == [0, 71]
+    assert torch.equal(tr.Linv[0], torch.eye(130, dtype=torch.float64, device=dev))
+
+
+def test_predict_from_cholesky_factor(dev):
+    """gp_predict_chol(L) (a caller holding a LAPACK factor) == gp_predict(L^-1) to rounding."""
+    from gladsgp_amd import kernels
+    rng = np.random.default_rng(9)
+    n, m, d, B = 700, 3000, 8, 2
+    X, Xs = rng.random((n, d)), rng.random((m, d))
+    betas = rng.uniform(0.5, 4, (B, d))
+    s = np.array([1.0, 1.7])
+    delta = np.array([1e-5, 1e-3])
+    W = rng.standard_normal((B, n))
+    G = kernels.gram(_t(X, dev), _t(betas, dev), _t(s, dev), _t(delta, dev))
+    L, info, _ = kernels.cholesky(G)
+    mean, var, info2 = kernels.predict_chol(L, _t(X, dev), _t(Xs, dev), _t(betas, dev),
+                                            _t(s, dev), _t(s, dev), _t(W, dev))
+    assert int(info.abs().sum()) == 0 and int(info2.abs().sum()) == 0
+    for b in range(B):
+        mr, vr = gp_ref.predict(X, Xs, W[b], betas[b], s[b], delta[b])
+        np.testing.assert_allclose(mean[b].cpu().numpy(), mr, rtol=0,
+                                   atol=1e-8 * max(1.0, np.abs(mr).max()))
+        np.testing.assert_allclose(var[b].cpu().numpy(), vr, rtol=0, atol=1e-9 * s[b])

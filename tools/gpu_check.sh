@@ -4,11 +4,11 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-run}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/${TAG}_pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?
 tail -5 gpurun_out/${TAG}_pytest.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python bench.py --steps 10 --warmup 3 ${BENCH_ARGS} > gpurun_out/${TAG}_bench.log 2>&1
 rc=$?
-tail -2 gpurun_out/${TAG}_bench.log
+tail -2 gpurun_out/${TAG}_bench.log | cut -c1-1500
 exit $rc
