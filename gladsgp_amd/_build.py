@@ -14,7 +14,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libgpfit.so")
 SOURCES = ["gram.hip", "chol.hip", "predict.hip", "linalg.hip", "profile.hip", "blas.hip",
-           "eig.hip", "comm.hip"]
+           "eig.hip", "comm.hip", "rng.hip"]
 # Per-file extra flags.  chol.hip: MFMA accumulators in VGPRs (not AGPRs) so the update
 # kernel, whose lookahead block calls the ~250-VGPR diagonal factor, keeps 2 waves/SIMD; and
 # 16-byte LDS reads (ds_read_b128) for the factor's broadcast rows.

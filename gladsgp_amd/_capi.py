@@ -67,6 +67,8 @@ SIGNATURES = {
     "gp_loglik": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                           c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,
                           c_void_p]),
+    "gp_realize": (c_int, [c_void_p, c_void_p, c_ll, ctypes.c_ulonglong, ctypes.c_ulonglong,
+                           c_void_p, c_void_p]),
     "gp_dgemm_ws_bytes": (c_ll, [c_int, c_int, c_int]),
     "gp_dgemm": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.c_double, c_void_p, c_int,
                          c_void_p, c_int, ctypes.c_double, c_void_p, c_int, c_void_p, c_ll,

@@ -219,7 +219,9 @@ GP_DEV void bcast_axpy(double (&y)[NB], const lds_double* V, double x) {
 //    64 elimination steps.  Step j: pivot p = A[j][j], t_c = A[j][c] / p (lanes c > j, else 0),
 //    A[r][c] -= A[r][j] t_c for r > j.  The trailing block stays symmetric, so A[r][j] is lane
 //    r's own row-j value: every lane writes w[j] to LDS row S[j] and the column comes back as
-//    16-byte broadcast reads (A[j+1][j], which the next pivot needs, goes by readlane).
+//    16-byte broadcast reads (A[j+1][j] = lane j+1's w[j], which the next pivot needs, goes by
+//    readlane).  Every row's factor comes from row j (the upper copy): the lower copies are
+//    only read back as L at the end, so rounding asymmetry between the two never feeds back.
 //    Critical path per column: readlane -> rcp + 2 Newton -> t -> one FMA; the broadcast reads
 //    are issued before the chain.  Lane c's column freezes after step c and then holds
 //    Lt[.][c] p_c, so L[r][c] = w[r] / sqrt(p_c).  t goes to LDS as the multiplier row M[j]
@@ -255,7 +257,12 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
       if constexpr (j + 1 < NB) {
         S[j * NB + lane] = wj;
         const double t = (lane > j) ? wj * rcp_nr(p) : 0.0;
-        w[j + 1] = fma(-readlane_f64(w[j + 1], j), t, w[j + 1]);
+        // row j+1's factor A[j+1][j] is taken from the same copy as every other row's: row j
+        // (lane j+1's w[j]), never lane j's own row j+1.  The trailing block is only
+        // symmetric up to rounding, and mixing the two copies fed that asymmetry back through
+        // the multipliers, amplified by |A|/p per step: on grid-like Grams whose pivots fall
+        // to ~1e-4 |A| within a few columns (BASELINE C1, d = 1) L was wrong from column ~10.
+        w[j + 1] = fma(-readlane_f64(wj, j + 1), t, w[j + 1]);
         M[j * NB + lane] = t;
         if constexpr (j + 2 < NB) bcast_axpy<j + 2>(w, &S[j * NB], t);
         // publish every DIAG_PE steps (and the last): the release store is a scheduling

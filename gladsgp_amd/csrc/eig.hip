@@ -1,5 +1,6 @@
 // Small dense symmetric eigensolver (cyclic Jacobi, one workgroup) — the r x r core of the
-// randomized SVD (src/svd.py:63 np.linalg.svd(B), B = Q^T X is r x ny with r = p + k <= 128):
+// randomized SVD (src/svd.py:63 np.linalg.svd(B), B = Q^T X is r x ny with r = p + k <= 1024;
+// the reference's calls use r = 25 (model.py:84), 100 (plot_PC_RMSE.py:91) and 2p when k=None):
 // SVD(B) is taken from the eigendecomposition of B B^T = U_B S^2 U_B^T (an r x r problem; the
 // r x ny products are MFMA GEMMs in blas.hip).
 //
@@ -14,7 +15,7 @@
 
 namespace {
 
-constexpr int kMaxR = 128;
+constexpr int kMaxR = 1024;   // LDS: rotations + pairing + sort keys, ~30 KB
 
 __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int r, int lda,
                                                      double* __restrict__ W,

@@ -20,10 +20,17 @@ each), with betaU (S, (d+1) P) reshaped C-order to (S, d+1, P), row 0 the dummy 
 ``pred_nugget`` selects whether 1/lamWs is part of the predictive prior variance (SEPIA's
 exact choice is not verifiable offline — SURVEY §8c — so it is a flag, default on).
 
-Differences from SEPIA, by design: ``.w`` is the posterior MEAN per (sample, PC) and ``.var``
-the marginal variance (SEPIA returns one joint random draw over the m_b x m_b covariance, which
-does not scale to m = 100k); ``sample_w`` draws marginal realisations.  All arithmetic runs
-in libgpfit (fp64); the (sample, PC) pairs are one batched Gram -> Cholesky/L^-1 -> predict.
+Differences from SEPIA, by design: by default ``.w`` is the posterior MEAN per (sample, PC)
+and ``.var`` the marginal variance (SEPIA returns one joint random draw over the m_b x m_b
+covariance of a call, which does not scale to m = 100k).  ``realize=True`` makes ``.w`` one
+marginal draw per (sample, point, PC) instead (gp_realize, Philox4x32-10 on the device, seeded
+by ``seed``), so the reference's quantile / coverage statistics over ``get_y()``
+(assess_all_models.py:489-500) keep the GP's predictive spread; ``.mean`` always holds the
+posterior mean.  ``.w`` is assignable, as the reference's callers do
+(``preds.w = preds.w.astype(np.float32)``, time_predictions.py:78, assess_all_models.py:490,
+513): ``get_y()`` then reconstructs from the assigned values and returns that dtype.  All
+arithmetic runs in libgpfit (fp64); the (sample, PC) pairs are one batched Gram ->
+Cholesky/L^-1 -> predict.
 """
 from __future__ import annotations
 
@@ -34,7 +41,7 @@ import torch
 
 from . import blas, kernels
 from . import dist as gdist
-from . import mcmc
+from . import mcmc, modelio
 from .blas import CM, gemm
 from .mcmc import ModelParams, SepiaParam  # noqa: F401  (re-exported for drop-in imports)
 
@@ -65,12 +72,19 @@ def _to_device_f64(x, device) -> torch.Tensor:
 
 
 class SimData:
-    """Simulation block: design, raw and standardised outputs, PCA basis (SEPIA sim_data)."""
+    """Simulation block: design, raw and standardised outputs, PCA basis (SEPIA sim_data).
+
+    ``t`` / ``y`` are host (numpy) arrays in the caller's dtype, as SEPIA's are — the
+    reference's drivers run numpy on them (``np.std(model.data.sim_data.y, ddof=1, axis=0)``,
+    time_predictions.py:65, assess_all_models.py:465); ``t_dev`` / ``y_dev`` are the float64
+    device copies every kernel reads."""
 
     def __init__(self, t_sim, y_sim, y_ind_sim, device):
         self.device = device
-        self.t = _to_device_f64(t_sim, device)
-        self.y = _to_device_f64(y_sim, device)
+        self.t_dev = _to_device_f64(t_sim, device)
+        self.y_dev = _to_device_f64(y_sim, device)
+        self._t_host = None if torch.is_tensor(t_sim) else np.asarray(t_sim)
+        self._y_host = None if torch.is_tensor(y_sim) else np.asarray(y_sim)
         self.y_ind = np.asarray(y_ind_sim)
         self.y_mean = None
         self.y_sd = None
@@ -78,8 +92,20 @@ class SimData:
         self.K = None          # (P, ny) basis
 
     @property
+    def t(self) -> np.ndarray:
+        if self._t_host is None:
+            self._t_host = self.t_dev.cpu().numpy()
+        return self._t_host
+
+    @property
+    def y(self) -> np.ndarray:
+        if self._y_host is None:
+            self._y_host = self.y_dev.cpu().numpy()
+        return self._y_host
+
+    @property
     def n(self) -> int:
-        return self.t.shape[0]
+        return self.t_dev.shape[0]
 
 
 class EmulatorData:
@@ -95,12 +121,12 @@ class EmulatorData:
         """y_std = (y - mu)/sd with mu/sd from the ensemble when not given (model.py:60-73)."""
         sd_ = self.sim_data
         if y_mean is None or y_sd is None:
-            mu, sd = blas.sim_stats(sd_.y, sd_threshold)
+            mu, sd = blas.sim_stats(sd_.y_dev, sd_threshold)
         else:
             mu = torch.as_tensor(_np(y_mean), dtype=F64, device=self.device).contiguous()
             sd = torch.as_tensor(_np(y_sd), dtype=F64, device=self.device).contiguous()
         sd_.y_mean, sd_.y_sd = mu, sd
-        sd_.y_std = blas.standardize(sd_.y, mu, sd)
+        sd_.y_std = blas.standardize(sd_.y_dev, mu, sd)
 
     def create_K_basis(self, K):
         """Set the PCA basis K (P x ny) — SEPIA create_K_basis (model.py:102)."""
@@ -141,7 +167,7 @@ class EmulatorModel:
         self.device = data.device
         self.w_hat_cm, lam = pc_weights(data)          # (n x P) column-major
         self.LamSim = lam
-        self.n, self.d = sd_.t.shape
+        self.n, self.d = sd_.t_dev.shape
         self.P = sd_.K.shape[0]
         # GPMSA default starting values, priors and steps (see gladsgp_amd.mcmc)
         self.params = ModelParams(self.d, self.P)
@@ -150,7 +176,7 @@ class EmulatorModel:
 
     # ---------------------------------------------------------------------------- sampling
     def _sampler(self) -> mcmc.GPUSampler:
-        return mcmc.GPUSampler(self.data.sim_data.t, self.w_hat.transpose(0, 1).contiguous(),
+        return mcmc.GPUSampler(self.data.sim_data.t_dev, self.w_hat.transpose(0, 1).contiguous(),
                                self.LamSim, self.params)
 
     def tune_step_sizes(self, n_burn, n_levels, prog=False, diagnostics=False,
@@ -199,33 +225,22 @@ class EmulatorModel:
         return {k: v[idx] for k, v in self.samples.items()}
 
     def save_model_info(self, path):
-        """Samples, current values and step sizes as ``path + '.npz'`` (plain arrays)."""
-        arrs = {f"samples_{k}": v for k, v in (self.samples or {}).items()}
-        for k in ModelParams.names:
-            p = getattr(self.params, k)
-            arrs[f"param_{k}"] = p.val
-            arrs[f"step_{k}"] = p.mcmcStepParam
-        np.savez(path if path.endswith(".npz") else path + ".npz", **arrs)
+        """Samples, current values and step sizes as ``path + '.npz'`` (plain arrays,
+        gladsgp_amd.modelio)."""
+        modelio.save_model_npz(path, self.samples,
+                               {k: getattr(self.params, k).val for k in ModelParams.names},
+                               {k: getattr(self.params, k).mcmcStepParam
+                                for k in ModelParams.names})
 
     def restore_model_info(self, path):
-        """Read ``path + '.npz'`` written by save_model_info (or an export of a SEPIA fit with
-        ``samples_<name>`` arrays, in SEPIA's ``(S,) + val_shape`` layout or flattened)."""
-        f = path if path.endswith(".npz") else path + ".npz"
-        samples = {}
-        with np.load(f, allow_pickle=False) as z:
-            for k in z.files:
-                if k.startswith("samples_"):
-                    v = np.asarray(z[k], dtype=np.float64)
-                    name = k[8:]
-                    if name in ModelParams.names and v.ndim >= 1:
-                        # (S,) + val_shape -> (S, prod(val_shape)), C order (betaU (S, (d+1) P))
-                        v = v.reshape(v.shape[0], -1)
-                    samples[name] = v
-                elif k.startswith("param_"):
-                    self.params[k[6:]] = z[k]
-                elif k.startswith("step_"):
-                    p = getattr(self.params, k[5:])
-                    p.mcmcStepParam = np.broadcast_to(z[k], p.val_shape).copy()
+        """Read ``path + '.npz'`` written by save_model_info or by
+        tools/export_sepia_samples.py from a SEPIA fit (gladsgp_amd.modelio)."""
+        samples, params, steps = modelio.load_model_npz(path)
+        for k, v in params.items():
+            self.params[k] = v
+        for k, v in steps.items():
+            p = getattr(self.params, k)
+            p.mcmcStepParam = np.broadcast_to(v, p.val_shape).copy()
         self.samples = samples or None
 
     # ------------------------------------------------------------------------- likelihood
@@ -238,7 +253,7 @@ class EmulatorModel:
         pr = self.params.values() if params is None else params
         samples = {k: np.asarray(pr[k]).reshape(1, -1) for k in self.param_names}
         beta, s, delta, _ = gp_params(samples, _np(self.LamSim), self.d, self.P, False)
-        X = self.data.sim_data.t
+        X = self.data.sim_data.t_dev
         G = kernels.gram(X, torch.as_tensor(beta[0], device=self.device),
                          torch.as_tensor(s[0], device=self.device),
                          torch.as_tensor(delta[0], device=self.device), batch=self.P)
@@ -302,12 +317,13 @@ class EmulatorPrediction:
 
     def __init__(self, model: EmulatorModel = None, samples: dict = None, t_pred=None,
                  pred_nugget: bool = True, ctx: gdist.Context | None = None,
-                 budget_bytes: int = 2 << 30, m_chunk: int = 0):
+                 budget_bytes: int = 2 << 30, m_chunk: int = 0, realize: bool = False,
+                 seed: int | None = None):
         if model is None or samples is None or t_pred is None:
             raise ValueError("EmulatorPrediction needs model, samples and t_pred")
         self.model = model
         dev = model.device
-        X = model.data.sim_data.t
+        X = model.data.sim_data.t_dev
         Xs = torch.as_tensor(_np(t_pred), dtype=F64, device=dev).reshape(-1, model.d)
         Xs = Xs.contiguous()
         beta, s, delta, sp = gp_params(samples, _np(model.LamSim), model.d, model.P,
@@ -331,32 +347,58 @@ class EmulatorPrediction:
         else:
             mean_l = torch.empty((0, self.m), dtype=F64, device=dev)
             var_l = torch.empty((0, self.m), dtype=F64, device=dev)
+        self.ctx = ctx
+        self.realized = bool(realize)
+        self.seed = int(np.random.SeedSequence().entropy & (2 ** 63 - 1)) if seed is None \
+            else int(seed)
+        self._w_dtype = np.dtype(np.float64)
         both = assemble_units(ctx, mean_l, var_l, len(units))
         if both is None:
-            self.w_dev = self.var_dev = None
+            self.mean_dev = self.w_dev = self.var_dev = None
             return
         mean_u, var_u = both
         # units are (s, j) in s-major order -> (S, P, m) -> (S, m, P)
-        self.w_dev = mean_u.reshape(S, P, self.m).permute(0, 2, 1).contiguous()
+        self.mean_dev = mean_u.reshape(S, P, self.m).permute(0, 2, 1).contiguous()
         self.var_dev = var_u.reshape(S, P, self.m).permute(0, 2, 1).contiguous()
+        self.w_dev = (kernels.realize(self.mean_dev, self.var_dev, self.seed) if self.realized
+                      else self.mean_dev)
 
     @property
     def w(self) -> np.ndarray:
-        """(S, m, P) posterior mean PC weights (numpy, as the reference consumes ``.w``)."""
-        return None if self.w_dev is None else self.w_dev.cpu().numpy()
+        """(S, m, P) PC weights as the reference consumes ``.w`` (numpy): the posterior mean,
+        or one marginal draw per entry with ``realize=True``, or whatever was assigned."""
+        return None if self.w_dev is None else self.w_dev.cpu().numpy().astype(self._w_dtype,
+                                                                              copy=False)
+
+    @w.setter
+    def w(self, value) -> None:
+        """Assign the PC weights ``get_y()`` reconstructs from (the reference casts them with
+        ``preds.w = preds.w.astype(np.float32)`` first): kept on the device as float64 copies of
+        the assigned values; ``get_y()`` returns the assigned dtype."""
+        a = np.asarray(value) if not torch.is_tensor(value) else value
+        if tuple(a.shape) != (self.S, self.m, self.P):
+            raise ValueError(f"w: expected shape {(self.S, self.m, self.P)}, got {tuple(a.shape)}")
+        self._w_dtype = np.dtype(a.dtype if not torch.is_tensor(a) else
+                                 torch.empty((), dtype=a.dtype).numpy().dtype)
+        self.w_dev = _to_device_f64(a, self.model.device)
+
+    @property
+    def mean(self) -> np.ndarray:
+        """(S, m, P) posterior mean of the PC weights."""
+        return None if self.mean_dev is None else self.mean_dev.cpu().numpy()
 
     @property
     def var(self) -> np.ndarray:
         return None if self.var_dev is None else self.var_dev.cpu().numpy()
 
     def get_mu_sigma(self):
-        return self.w, self.var
+        return self.mean, self.var
 
-    def sample_w(self, rng=None) -> np.ndarray:
-        """One marginal realisation per (sample, point, PC): mean + sqrt(var) N(0, 1)."""
-        rng = np.random.default_rng() if rng is None else rng
-        z = rng.standard_normal(self.w.shape)
-        return self.w + np.sqrt(np.maximum(self.var, 0.0)) * z
+    def sample_w(self, seed: int | None = None, offset: int = 1) -> np.ndarray:
+        """A fresh marginal realisation per (sample, point, PC), mean + sqrt(var) N(0, 1), on
+        the device (gp_realize; ``offset`` selects an independent stream for one seed)."""
+        seed = self.seed if seed is None else int(seed)
+        return kernels.realize(self.mean_dev, self.var_dev, seed, offset).cpu().numpy()
 
     def error_draws(self, rng=None, per_point: bool = True) -> np.ndarray:
         """Standardised residual error of the reference's predictions: one N(0, 1/sqrt(lamWOs_s))
@@ -368,26 +410,64 @@ class EmulatorPrediction:
         return rng.standard_normal((self.S, cols)) / np.sqrt(self.lamWOs)[:, None]
 
     def get_y(self, std: bool = False, w=None, add_error: bool = False, rng=None,
-              per_point: bool = True) -> np.ndarray:
+              per_point: bool = True, ctx="inherit", gather: bool = True):
         """Field reconstruction y = (w K) sd + mu, shape (S, m, ny) — SEPIA get_y().
 
         ``add_error`` adds the reference's PC-truncation error term (error_draws, times sd_y
-        in physical units): y = (w K + e) sd + mu, one scalar e per (sample[, point])."""
+        in physical units): y = (w K + e) sd + mu, one scalar e per (sample[, point]).
+
+        Distributed (``ctx``, by default the prediction's; SURVEY §8e "field reconstruction"):
+        rank 0's w (and error draws) are broadcast, rank r reconstructs the output columns
+        ``shard_range(ny, r, N)`` with its slice of K, and with ``gather`` rank 0 receives the
+        whole (S, m, ny) field (other ranks None); ``gather=False`` returns every rank's own
+        (S, m, ny_r) column block (``self.y_cols`` holds its range).
+        """
         sd_ = self.model.data.sim_data
-        wd = self.w_dev if w is None else torch.as_tensor(w, dtype=F64,
-                                                            device=self.model.device)
-        S, m, P = wd.shape
+        dev = self.model.device
+        ctx = self.ctx if isinstance(ctx, str) else ctx
+        dist_on = ctx is not None and ctx.distributed
+        S, m, P = self.S, self.m, self.P
+        if dist_on:
+            flag = torch.tensor([1 if self._w_dtype == np.float32 else 0], device=dev)
+            gdist.broadcast_(ctx, flag)
+            f32 = bool(flag.item()) and w is None
+            if ctx.rank == 0:
+                wd = (self.w_dev if w is None else _to_device_f64(w, dev)).contiguous()
+            else:
+                wd = torch.empty((S, m, P), dtype=F64, device=dev)
+            gdist.broadcast_(ctx, wd)
+            ny = sd_.K.shape[1]
+            c0, c1 = gdist.shard_range(ny, ctx.rank, ctx.world)
+        else:
+            f32 = w is None and self._w_dtype == np.float32
+            wd = self.w_dev if w is None else _to_device_f64(w, dev)
+            c0, c1 = 0, sd_.K.shape[1]
+        out_dtype = np.float32 if f32 else np.float64
+        self.y_cols = (c0, c1)
+        K = sd_.K if (c0, c1) == (0, sd_.K.shape[1]) else sd_.K[:, c0:c1].contiguous()
         Wc = CM.of_rowmajor(wd.reshape(S * m, P).contiguous())   # (P x S m)
-        Kc = CM.of_rowmajor(sd_.K)                               # (ny x P)
-        Yc = gemm(False, False, Kc, Wc)                          # (ny x S m) = (w K)^T
-        y = Yc.t[: S * m, : sd_.K.shape[1]]                      # (S m, ny) row-major
+        Kc = CM.of_rowmajor(K)                                   # (ny_r x P)
+        Yc = gemm(False, False, Kc, Wc)                          # (ny_r x S m) = (w K)^T
+        y = Yc.t[: S * m, : c1 - c0]                             # (S m, ny_r) row-major
         if add_error:
-            e = torch.as_tensor(self.error_draws(rng, per_point), dtype=F64, device=y.device)
+            cols = m if per_point else 1
+            if not dist_on or ctx.rank == 0:
+                e = torch.as_tensor(self.error_draws(rng, per_point), dtype=F64, device=dev)
+            else:
+                e = torch.empty((S, cols), dtype=F64, device=dev)
+            if dist_on:
+                gdist.broadcast_(ctx, e)
             e = e.expand(S, m) if e.shape[1] == 1 else e
             y = y + e.reshape(S * m, 1)                          # one scalar per row
         if not std:
-            y = blas.standardize(y.contiguous(), sd_.y_mean, sd_.y_sd, inverse=True)
-        return y.reshape(S, m, -1).cpu().numpy()
+            mu, sd = sd_.y_mean[c0:c1].contiguous(), sd_.y_sd[c0:c1].contiguous()
+            y = blas.standardize(y.contiguous(), mu, sd, inverse=True)
+        if dist_on and gather:
+            counts = [gdist.shard_range(sd_.K.shape[1], r, ctx.world) for r in range(ctx.world)]
+            y = gdist.gather_cols(ctx, y.contiguous(), [b - a for a, b in counts])
+            if y is None:
+                return None
+        return y.reshape(S, m, -1).cpu().numpy().astype(out_dtype, copy=False)
 
 
 def assemble_units(ctx, mean_l: torch.Tensor, var_l: torch.Tensor, n_units: int):
@@ -406,11 +486,17 @@ def assemble_units(ctx, mean_l: torch.Tensor, var_l: torch.Tensor, n_units: int)
     allb = gdist.gather_rows(ctx, both, counts)
     if allb is None:
         return None
+    allb = unit_order(allb, n_units, world)
+    return allb[:, 0], allb[:, 1]
+
+
+def unit_order(rank_major: torch.Tensor, n_units: int, world: int) -> torch.Tensor:
+    """Rows gathered rank by rank (rank r's round-robin units shard_units(n_units, r, world) in
+    order) -> rows in unit order."""
     order = np.concatenate([gdist.shard_units(n_units, r, world) for r in range(world)])
     inv = np.empty_like(order)
     inv[order] = np.arange(len(order))
-    allb = allb[torch.as_tensor(inv, device=allb.device)]
-    return allb[:, 0], allb[:, 1]
+    return rank_major[torch.as_tensor(inv, device=rank_major.device)]
 
 
 # SEPIA-compatible alias for drop-in call sites

@@ -445,3 +445,18 @@ def predict_chol(L: torch.Tensor, X, Xs, beta, s, s_pred, w, m_chunk: int = 0,
                mean.data_ptr(), var.data_ptr(), m, batch, info.data_ptr(), ws.data_ptr(),
                ws.numel(), int(m_chunk), _stream(dev))
     return mean, var, info
+
+
+def realize(mean: torch.Tensor, var: torch.Tensor, seed: int, offset: int = 0,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """One marginal draw per entry, mean + sqrt(max(var, 0)) z with z from Philox4x32-10 keyed
+    by ``seed`` at counter offset ``offset`` (gp_realize); deterministic per (seed, offset)."""
+    _check_device(mean, "mean")
+    if mean.dtype != F64 or var.dtype != F64 or mean.shape != var.shape:
+        raise TypeError("mean / var must be float64 tensors of one shape")
+    mean_c, var_c = mean.contiguous(), var.contiguous()
+    out = torch.empty_like(mean_c) if out is None else out
+    _capi.call("gp_realize", mean_c.data_ptr(), var_c.data_ptr(), mean_c.numel(),
+               int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), out.data_ptr(),
+               _stream(mean.device))
+    return out

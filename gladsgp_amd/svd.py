@@ -12,7 +12,13 @@ Build (all arithmetic in libgpfit, fp64):
     ill-conditioned, so the first pass factors ``Y^T Y + s I`` (s = 11 (n r + r(r+1)) u ||Y||^2,
     a trace bound), two plain CholeskyQR passes then restore orthogonality to ~u.  The
     Cholesky + inverse is ``gp_potrf_inv``;
-  * ``svd(B)`` comes from the Jacobi eigendecomposition of ``B B^T`` (``gp_syevj``, r <= 128):
+  * a rank-deficient ``Y`` (e.g. ``init_model``'s ``r = min(25, n, ny)`` on a column-centred
+    ensemble of n <= 25 runs, rank <= n - 1) makes a CholeskyQR pass fail; numpy's Householder
+    QR still returns an orthonormal Q there.  The fallback: eigen-basis of ``Y^T Y``
+    (gp_syevj) for the numerically nonzero directions, CholeskyQR2 to restore orthogonality,
+    and a seeded orthonormal completion of the null directions (B = Q^T X sees only range(X)
+    there, so any completion gives the reference's U, S, Vh up to the zero singular values);
+  * ``svd(B)`` comes from the Jacobi eigendecomposition of ``B B^T`` (``gp_syevj``, r <= 1024):
     ``S = sqrt(eig)``, ``V^T = S^-1 U_B^T B``.
 Singular vectors are unique up to sign (and rotation inside clusters); tests compare signed.
 The reference's ``return_error`` bound is always 0 because ``S`` is truncated before ``S[p]``
@@ -49,10 +55,44 @@ def _chol_qr(Y: CM, shift: bool) -> CM:
 
 
 def orthonormalize(Y: CM) -> CM:
-    """Orthonormal basis of range(Y) (n x r, r <= 128): shifted CholeskyQR3."""
-    Q = _chol_qr(Y, shift=True)
-    Q = _chol_qr(Q, shift=False)
-    return _chol_qr(Q, shift=False)
+    """Orthonormal n x r basis containing range(Y) (r <= n): shifted CholeskyQR3, or the
+    rank-revealing fallback when Y is (numerically) rank deficient."""
+    try:
+        Q = _chol_qr(Y, shift=True)
+        Q = _chol_qr(Q, shift=False)
+        return _chol_qr(Q, shift=False)
+    except ValueError:       # a pass hit a non-positive pivot: rank(Y) < r
+        return _orthonormalize_deficient(Y)
+
+
+def _orthonormalize_deficient(Y: CM, rel_tol: float = 1e-10, seed: int = 0x5EED) -> CM:
+    n, r = Y.rows, Y.cols
+    dev = Y.t.device
+    G = gemm(True, False, Y, Y)                              # r x r = Y^T Y
+    lam, V, _ = syevj(G, want_sqrt=False)                    # descending
+    lam_h = lam.cpu().numpy()
+    k = int(np.sum(lam_h > rel_tol * max(lam_h[0], 0.0))) if r else 0
+    parts = []
+    if k:
+        Vk = CM(V.t[:k], r, k, V.ld)                         # first k eigenvectors
+        Q1 = gemm(False, False, Y, Vk)                       # n x k, cond <= rel_tol^-1/2
+        Q1 = _chol_qr(_chol_qr(_chol_qr(Q1, shift=True), shift=False), shift=False)
+        parts.append(Q1)
+    if k < r:
+        # seeded Gaussian columns, projected off range(Q1) twice, then CholeskyQR2
+        z = np.random.default_rng(seed).standard_normal((r - k, n))
+        Z = CM.of_rowmajor(torch.as_tensor(z, dtype=torch.float64, device=dev))  # n x (r-k)
+        if k:
+            for _ in range(2):
+                P = gemm(True, False, parts[0], Z)           # k x (r-k)
+                gemm(False, False, parts[0], P, alpha=-1.0, beta=1.0, C=Z)
+        parts.append(_chol_qr(_chol_qr(Z, shift=False), shift=False))
+    Q = CM.empty(n, r, dev)
+    c = 0
+    for part in parts:
+        Q.t[c:c + part.cols, :n] = part.t[: part.cols, :n]
+        c += part.cols
+    return Q
 
 
 def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=None):
@@ -71,8 +111,8 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
     if k is None:
         k = p
     r = p + k
-    if r > 128:
-        raise ValueError("randomized_svd: p + k must be <= 128 (Jacobi core)")
+    if r > 1024:
+        raise ValueError("randomized_svd: p + k must be <= 1024 (Jacobi core)")
     if omega is None:
         omega = np.random.normal(size=(n_cols, r)).astype(np.float32)
     Om = torch.as_tensor(np.asarray(omega) if not torch.is_tensor(omega) else omega,
@@ -83,6 +123,10 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
     for _ in range(q):
         Z = gemm(False, False, Xc, Y)    # (n_cols x r) = X^T Y
         Y = gemm(True, False, Xc, Z)     # (m_rows x r) = X X^T Y
+    if r > m_rows:
+        # more test vectors than rows: range(Y) is all of R^m_rows (numpy's reduced QR gives
+        # an m_rows x m_rows Q), so keep m_rows of them
+        Y = CM(Y.t[:m_rows], m_rows, m_rows, Y.ld)
     Q = orthonormalize(Y)
     B = gemm(True, True, Q, Xc)      # (r x n_cols) = Q^T X
     G = gemm(False, True, B, B)      # (r x r) = B B^T

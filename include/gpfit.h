@@ -220,6 +220,16 @@ int gp_loglik(const double* X, int n, int d, int ldx, const double* beta, int ld
               const double* s, const double* delta, const double* w, int ldw, int batch,
               void* ws, long long ws_bytes, double* ll, int* info, hipStream_t stream);
 
+/*
+ * One marginal realisation per entry: out[i] = mean[i] + sqrt(max(var[i], 0)) z_i, z_i ~ N(0,1)
+ * from counter-based Philox4x32-10 keyed by `seed` (counter (i/2, offset); Box-Muller pairs),
+ * so the draws depend only on (seed, offset, i).  out may alias mean.  The opt-in realize mode
+ * of the prediction: SepiaEmulatorPrediction's .w is a random draw of the PC weights, whose
+ * spread the reference's quantile / coverage statistics use (assess_all_models.py:489-500).
+ */
+int gp_realize(const double* mean, const double* var, long long N, unsigned long long seed,
+               unsigned long long offset, double* out, hipStream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Fit-side dense kernels (src/model.py init_model and src/svd.py randomized_svd).
  * ---------------------------------------------------------------------------------------- */
@@ -254,7 +264,7 @@ int gp_shift_diag(double* A, int r, int lda, double factor, hipStream_t stream);
 int gp_rowscale(double* M, int rows, int cols, int ld, const double* f, int inv,
                 hipStream_t stream);
 
-/* Symmetric eigendecomposition A = V diag(W) V^T by cyclic Jacobi (r <= 128, one workgroup),
+/* Symmetric eigendecomposition A = V diag(W) V^T by cyclic Jacobi (r <= 1024, one workgroup),
  * eigenvalues descending (want_sqrt = 1: W = sqrt(max(eig, 0)), the singular values when
  * A = B B^T); A is destroyed.  `sweeps` (device int, may be NULL) receives the sweep count.
  * The r x r core of np.linalg.svd(B) in src/svd.py:63 (via B B^T). */

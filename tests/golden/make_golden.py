@@ -15,6 +15,10 @@ Writes only data (.npz / .json / .csv) into tests/golden/:
   imported from the read-only reference tree, on a seeded float32 matrix with
   ``np.random.seed(123)`` (p=8, k=None, q=1) and (p=25, k=0, q=1), together with the Gaussian
   test matrices it drew, so the oracle restatement can be checked exactly.
+* ``svd_ref_deficient.npz`` — the reference's ``randomized_svd`` on column-centred (hence
+  rank <= n - 1) float32 ensembles of n = 16, 20, 25 runs with ``init_model``'s
+  ``r = min(25, n, ny)``, k = 0, q = 1 (``src/model.py:84``; ``test_install.sh`` uses
+  ``--nsim 16``), seeded, with the Gaussian test matrices it drew.
 * ``c2_golden.npz`` — oracle GP outputs on the real 512x8 design (C2 recipe) at
   256 test points: Gram spot values, logdet, mean, var, nll.
 """
@@ -92,6 +96,33 @@ def svd_reference(ref: str) -> None:
     print("svd golden written")
 
 
+def svd_reference_deficient(ref: str) -> None:
+    spec = importlib.util.spec_from_file_location("ref_svd", os.path.join(ref, "src", "svd.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = {}
+    ny = 400
+    for n in (16, 20, 25):
+        rng = np.random.default_rng(100 + n)
+        t = rng.random((n, 4))
+        modes = rng.standard_normal((8, ny)) * (0.7 ** np.arange(8))[:, None]
+        coef = np.stack([np.sin(2 * np.pi * t @ rng.uniform(0, 1, 4) + k) for k in range(8)], 1)
+        y = (3.0 + coef @ modes + 1e-2 * rng.standard_normal((n, ny))).astype(np.float32)
+        mu = np.mean(y, axis=0)                      # src/model.py:60-72
+        sd = np.std(y, ddof=1, axis=0)
+        sd[sd < 1e-6] = 1e-6
+        y_std = (y - mu) / sd
+        r = min(25, *y_std.shape)
+        np.random.seed(1000 + n)
+        U, S, Vh = mod.randomized_svd(y_std, r, k=0, q=1)
+        np.random.seed(1000 + n)
+        omega = np.random.normal(size=(ny, r)).astype(np.float32)
+        out.update({f"n{n}_y_std": y_std, f"n{n}_U": U, f"n{n}_S": S, f"n{n}_Vh": Vh,
+                    f"n{n}_omega": omega})
+    np.savez_compressed(os.path.join(HERE, "svd_ref_deficient.npz"), **out)
+    print("rank-deficient svd golden written")
+
+
 def c2_golden() -> None:
     X = np.loadtxt(os.path.join(HERE, "synthetic_train_standard.csv"), delimiter=",",
                    skiprows=1, comments=None)
@@ -121,6 +152,7 @@ def main() -> None:
     copy_designs(args.reference)
     notebook_known_answer(args.reference)
     svd_reference(args.reference)
+    svd_reference_deficient(args.reference)
     c2_golden()
 
 

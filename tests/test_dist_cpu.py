@@ -46,7 +46,38 @@ def _worker(rank, world, port, results):
         else:
             ok_g = out is None
         t = gdist.max_over_ranks(ctx, 1.0 + rank)
-        results[rank] = (ok_b, ok_g, t)
+        # strong-scaled single-output GP (bench C3): contiguous test-point blocks
+        # of (mean, var) as (2, m_r), gathered to rank 0 in rank order
+        m_tot = 1001
+        lo, hi = gdist.shard_range(m_tot, rank, world)
+        counts = [b - a for a, b in (gdist.shard_range(m_tot, r, world) for r in range(world))]
+        j = torch.arange(lo, hi, dtype=torch.float64)
+        blk = torch.stack([j * 2.0, -j])
+        full = gdist.gather_cols(ctx, blk, counts)
+        if rank == 0:
+            ref = torch.arange(m_tot, dtype=torch.float64)
+            ok_s = bool(full.shape == (2, m_tot) and torch.equal(full[0], 2 * ref)
+                        and torch.equal(full[1], -ref))
+        else:
+            ok_s = full is None
+        # field reconstruction: all-gather of w rows, then a column block of K per rank
+        S_m, P, ny = 5, 3, 17
+        rows = gdist.shard_units(S_m, rank, world)
+        w_loc = torch.tensor([[10.0 * u + q for q in range(P)] for u in rows],
+                             dtype=torch.float64).reshape(len(rows), P)
+        rc = [len(gdist.shard_units(S_m, r, world)) for r in range(world)]
+        w_all = gdist.all_gather_rows(ctx, w_loc, rc)
+        order = np.concatenate([gdist.shard_units(S_m, r, world) for r in range(world)])
+        w_ref = torch.tensor([[10.0 * u + q for q in range(P)] for u in order],
+                             dtype=torch.float64)
+        ok_a = bool(torch.equal(w_all, w_ref))
+        c0, c1 = gdist.shard_range(ny, rank, world)
+        Kfull = torch.arange(P * ny, dtype=torch.float64).reshape(P, ny)
+        y_loc = w_all @ Kfull[:, c0:c1]            # stands in for the device GEMM
+        ycnt = [b - a for a, b in (gdist.shard_range(ny, r, world) for r in range(world))]
+        y = gdist.gather_cols(ctx, y_loc.contiguous(), ycnt)
+        ok_y = bool(torch.equal(y, w_all @ Kfull)) if rank == 0 else y is None
+        results[rank] = (ok_b, ok_g, t, ok_s, ok_a, ok_y)
     finally:
         dist.destroy_process_group()
 
@@ -68,6 +99,6 @@ def test_gloo_world2_broadcast_gather_max():
     results = mgr.dict()
     mp.spawn(_worker, args=(world, port, results), nprocs=world, join=True)
     for r in range(world):
-        ok_b, ok_g, t = results[r]
-        assert ok_b and ok_g
+        ok_b, ok_g, t, ok_s, ok_a, ok_y = results[r]
+        assert ok_b and ok_g and ok_s and ok_a and ok_y
         assert t == 2.0

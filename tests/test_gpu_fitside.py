@@ -116,3 +116,70 @@ def test_randomized_svd_field(dev):
     # singular values come from eig(B B^T): absolute error ~ eps S_max^2 / S_i (stated model)
     tol = 1e-9 * So + 1e-12 * So[0] ** 2 / So
     assert np.all(np.abs(S - So) <= tol)
+
+
+@pytest.mark.parametrize("n", [16, 20, 25])
+def test_randomized_svd_rank_deficient_vs_reference(dev, golden_dir, n):
+    """init_model's r = min(25, n, ny) on a column-centred ensemble of n <= 25 runs (rank
+    <= n - 1: a CholeskyQR pass hits a zero pivot): the reference's own src/svd.py outputs
+    (tests/golden/svd_ref_deficient.npz) vs the GPU with the same Omega."""
+    from gladsgp_amd.svd import randomized_svd
+    g = np.load(os.path.join(golden_dir, "svd_ref_deficient.npz"))
+    y_std = g[f"n{n}_y_std"]
+    r = min(25, *y_std.shape)
+    U, S, Vh = randomized_svd(y_std, r, k=0, q=1, omega=g[f"n{n}_omega"], device=dev)
+    assert U.shape == (n, r) and S.shape == (r,) and Vh.shape == (r, y_std.shape[1])
+    assert np.all(np.isfinite(U)) and np.all(np.isfinite(S)) and np.all(np.isfinite(Vh))
+    np.testing.assert_allclose(U.T @ U, np.eye(r), atol=1e-10)
+    S_ref = g[f"n{n}_S"]
+    # the n - 1 nonzero singular values (float32 reference), the last one numerically zero
+    np.testing.assert_allclose(S[: n - 1], S_ref[: n - 1], rtol=2e-4, atol=1e-4 * S_ref[0])
+    assert S[-1] <= 1e-6 * S[0]
+    # exact SVD of the (rank n-1) input: the GPU's fp64 values are tight
+    S_ex = np.linalg.svd(y_std.astype(np.float64), compute_uv=False)
+    np.testing.assert_allclose(S[: n - 1], S_ex[: n - 1], rtol=1e-8)
+    # leading, well-separated singular vectors agree with the reference up to sign
+    U_ref, Vh_ref = g[f"n{n}_U"], g[f"n{n}_Vh"]
+    for i in range(3):
+        if (S_ref[i] - S_ref[i + 1]) > 1e-2 * S_ref[0]:
+            sg = np.sign(U[:, i] @ U_ref[:, i])
+            np.testing.assert_allclose(sg * U[:, i], U_ref[:, i], atol=1e-3)
+            np.testing.assert_allclose(sg * Vh[i], Vh_ref[i], atol=1e-3)
+    # reconstruction of the input from the rank-r factors
+    err = np.linalg.norm(y_std - (U * S) @ Vh) / np.linalg.norm(y_std)
+    assert err < 1e-6
+
+
+def test_init_model_small_ensemble(dev, tmp_path):
+    """init_model at the reference's test_install.sh size (--nsim 16): no failure, finite
+    basis, PC weights of the GPU basis match the oracle."""
+    from gladsgp_amd import model as gm
+    rng = np.random.default_rng(16)
+    t = rng.random((16, 8))
+    y = (2.0 + np.sin(2 * np.pi * t @ rng.uniform(0, 1, 8))[:, None]
+         * rng.standard_normal((1, 300)) + 0.1 * rng.standard_normal((16, 300)))
+    data, model = gm.init_model(t.astype(np.float32), y.astype(np.float32), "tiny", 5,
+                                data_dir=str(tmp_path), device=dev, verbose=False)
+    K = data.sim_data.K.cpu().numpy()
+    assert K.shape == (5, 300) and np.all(np.isfinite(K))
+    ystd = data.sim_data.y_std.cpu().numpy()
+    np.testing.assert_allclose(model.w_hat.cpu().numpy(), gp_ref.pc_weights(ystd, K),
+                               atol=1e-7)
+
+
+@pytest.mark.parametrize("p,k", [(100, None), (150, 0)])
+def test_randomized_svd_large_rank(dev, p, k):
+    """p + k beyond the old 128 cap (the reference's default k=None doubles p; plot_PC_RMSE.py
+    uses p = min(100, n)): 200 x 3000 input, against numpy with the same Omega."""
+    from gladsgp_amd.svd import randomized_svd
+    rng = np.random.default_rng(p)
+    X = rng.standard_normal((400, 60)) @ rng.standard_normal((60, 3000)) \
+        + 0.01 * rng.standard_normal((400, 3000))
+    r = p + (p if k is None else k)
+    om = rng.standard_normal((3000, r)).astype(np.float32)
+    U, S, Vh = randomized_svd(X, p, k=k, q=1, omega=om, device=dev)
+    assert U.shape == (400, p) and S.shape == (p,) and Vh.shape == (p, 3000)
+    _, So, _ = gp_ref.randomized_svd(X, p, k=k, q=1, omega=om)
+    tol = 1e-9 * So + 1e-12 * So[0] ** 2 / So
+    assert np.all(np.abs(S - So) <= tol)
+    np.testing.assert_allclose(U.T @ U, np.eye(p), atol=1e-10)

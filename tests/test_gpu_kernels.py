@@ -460,3 +460,27 @@ def test_predict_from_cholesky_factor(dev):
         np.testing.assert_allclose(mean[b].cpu().numpy(), mr, rtol=0,
                                    atol=1e-8 * max(1.0, np.abs(mr).max()))
         np.testing.assert_allclose(var[b].cpu().numpy(), vr, rtol=0, atol=1e-9 * s[b])
+
+
+@pytest.mark.parametrize("n,ell", [(64, 0.05), (64, 0.2), (300, 0.05), (1000, 0.1)])
+def test_cholesky_grid_gram_ill_conditioned(dev, n, ell):
+    """Regression: 1-D grid Grams (BASELINE C1's shape, x = linspace(1/8, 7/8, n)) whose
+    Schur-complement pivots fall to ~1e-4 |A| within a few columns.  Round 1's diagonal factor
+    mixed the two rounding-level copies of the symmetric trailing block and lost L from column
+    ~10 (kappa ~1e6); checked here against numpy at kappa up to ~1e8."""
+    from gladsgp_amd import kernels
+    x = np.linspace(1 / 8, 7 / 8, n).reshape(-1, 1)
+    s, beta, delta = gp_ref.gpmodule_theta_to_kernel([0.3, ell], 1e-3)
+    G = gp_ref.gram_ardse(x, beta, s, delta)
+    L_ref = np.linalg.cholesky(G)
+    ch = kernels.cholesky_inverse(kernels.gram(_t(x, dev), _t(beta, dev), s, delta))
+    L, info, logdet = kernels.cholesky(kernels.gram(_t(x, dev), _t(beta, dev), s, delta))
+    assert int(ch.info[0]) == 0 and int(info[0]) == 0
+    for Lg in (ch.L[0].cpu().numpy(), L[0].cpu().numpy()):
+        assert np.linalg.norm(Lg @ Lg.T - G) / np.linalg.norm(G) <= 1e-13
+        kappa = np.linalg.cond(G)
+        assert np.max(np.abs(Lg - L_ref)) <= 1e-16 * kappa * np.abs(L_ref).max() * 10
+    np.testing.assert_allclose(float(ch.logdet[0]), 2 * np.sum(np.log(np.diag(L_ref))),
+                               rtol=1e-10)
+    Li = ch.Linv[0].cpu().numpy()
+    assert np.max(np.abs(Li @ L_ref - np.eye(n))) <= 1e-16 * np.linalg.cond(G) * 100
