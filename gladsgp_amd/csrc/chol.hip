@@ -233,6 +233,9 @@ GP_DEV void bcast_axpy(double (&y)[NB], const lds_double* V, double x) {
 // the sweep), M in U's (U is written after the barrier that ends both sweeps).
 // noinline: inlined into a kernel that also has rolled loops, the 64-step straight-line sweep
 // sends LLVM's CodeGenPrepare quadratic (minutes of compile time); as a callee it compiles alone.
+// TAG: one instantiation per caller family (the sweep's 2-wave/SIMD kernels, the persistent
+// 1-wave/SIMD one), so each is register-allocated for its own occupancy.
+template <int TAG>
 __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out) {
   LdsSmem& sm = *(LdsSmem*)&g_sm;
   const int tid = threadIdx.x;
@@ -314,6 +317,166 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
   return f;
 }
 
+// ---- Blocked 64x64 factor + inverse (the persistent chain's diagonal step) -------------------
+// Same contract as diag_factor_inv (T = sm.As full symmetric [row][col] with identity padding
+// past nb; on return T = L, U = sm.Bs = L^-1, both lower with zero upper), on 16 x 16 blocks:
+//   for b = 0..3:  leaf16(b)                        wave 0: L_bb, Dinv_b = L_bb^-1
+//                  L_rb = A_rb Dinv_b^T (r > b)     waves 1-3, one MFMA block each
+//                  A_rs -= L_rb L_sb^T (b < s <= r) wave 0 takes (b+1, b+1) and goes straight on
+//                                                   to the next leaf; waves 1-3 the rest
+//   X_rc = -Dinv_r sum_{k=c}^{r-1} L_rk X_kc        wave c builds column block c of L^-1
+// The leaf is the 16-column symmetric elimination of diag_factor_inv held in ONE wave's
+// registers (lanes 0-15 = columns of A, lanes 16-31 = columns of I for the inverse, same row
+// operations), the broadcasts are readlanes instead of LDS round trips, and every block
+// product is 4 v_mfma_f64_16x16x4.
+
+// acc += (negA ? -A : A) B over one 16 x 16 x 16 block; A(i,k) = Ab[i*ai + k*ak],
+// B(k,c) = Bb[k*bk + c*bc]  (C layout: lane l, reg q holds C[(l >> 4) + 4q][l & 15]).
+GP_DEV void mm16(f64x4& acc, const lds_double* Ab, int ai, int ak, const lds_double* Bb, int bk,
+                 int bc, bool negA) {
+  const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    double a = Ab[i * ai + (k0 + kk) * ak];
+    const double b = Bb[(k0 + kk) * bk + i * bc];
+    acc = mfma16x16x4(negA ? -a : a, b, acc);
+  }
+}
+GP_DEV f64x4 ld16(const lds_double* Cb) {          // row-major block, pitch LP
+  const int lane = threadIdx.x & 63;
+  f64x4 a;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = Cb[((lane >> 4) + 4 * q) * LP + (lane & 15)];
+  return a;
+}
+GP_DEV void st16(lds_double* Cb, const f64x4& a, double sg) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Cb[((lane >> 4) + 4 * q) * LP + (lane & 15)] = sg * a[q];
+}
+
+// One wave: factor + invert the 16 x 16 block at (o, o).  Writes L_bb into T's block and
+// Dinv_b into U's block (lower, zero upper); returns the first failing pivot (1-based, tile
+// index) among rows < nb, or 0; adds sum log pivots (rows < nb) to lg.
+GP_DEV int leaf16(lds_double* T, lds_double* U, int o, int nb, double& lg) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15;
+  const bool fac = lane < 16;
+  double v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = fac ? T[(o + r) * LP + o + c] : (r == c ? 1.0 : 0.0);
+  double rsq[16];
+  double mypiv = 1.0;
+  static_for<0, 16, 1>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    const double p = readlane_f64(v[j], j);
+    mypiv = (c == j) ? p : mypiv;
+    const double rp = rcp_nr(p);
+    // factor lanes: t_c = A[j][c] / p for c > j (columns <= j are final); inverse lanes:
+    // B[j][c] / p.  Row r's factor A[r][j] is lane r's own row-j value (the upper copy).
+    const double y = (fac && c <= j) ? 0.0 : v[j] * rp;
+    static_for<j + 1, 16, 1>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      v[r] = fma(-readlane_f64(v[j], r), y, v[r]);
+    });
+    rsq[j] = p;
+  });
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rsq[r] = rsqrt_nr(rsq[r]);
+  const double myrs = rsqrt_nr(mypiv);
+  if (lane < 32) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (fac)
+        T[(o + r) * LP + o + c] = r > c ? v[r] * myrs : (r == c ? mypiv * myrs : 0.0);
+      else
+        U[(o + r) * LP + o + c] = r >= c ? v[r] * rsq[r] : 0.0;
+    }
+  }
+  const bool ok = !(lane < 16 && o + c < nb) || (mypiv > 0.0 && isfinite(mypiv));
+  const unsigned long long bad = __ballot(!ok);
+  double l = (lane < 16 && o + c < nb) ? log(mypiv) : 0.0;
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) l += __shfl_xor(l, off, 64);
+  lg += readlane_f64(l, 0);
+  return bad ? o + __ffsll((long long)bad) : 0;
+}
+
+GP_DEV int diag_factor_blk(int nb, double* ld_out) {
+  LdsSmem& sm = *(LdsSmem*)&g_sm;
+  lds_double* T = sm.As;
+  lds_double* U = sm.Bs;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int fail = 0;
+  double lg = 0.0;
+  static_for<0, 4, 1>([&](auto Bk) {
+    constexpr int b = decltype(Bk)::value;
+    if (w == 0) {
+      const int f = leaf16(T, U, 16 * b, nb, lg);
+      if (!fail) fail = f;
+    }
+    __syncthreads();
+    if constexpr (b < 3) {
+      // panel: L_rb = A_rb Dinv_b^T, r = b + w
+      if (w >= 1 && b + w <= 3) {
+        const int r = b + w;
+        f64x4 acc = zero4();
+        mm16(acc, T + 16 * r * LP + 16 * b, LP, 1, U + 16 * b * LP + 16 * b, 1, LP, false);
+        st16(T + 16 * r * LP + 16 * b, acc, 1.0);
+      }
+      __syncthreads();
+      // trailing update of step b: (b+1, b+1) by wave 0, the other lower blocks by waves 1-3
+      auto upd = [&](int r, int s2) {
+        f64x4 acc = ld16(T + 16 * r * LP + 16 * s2);
+        mm16(acc, T + 16 * r * LP + 16 * b, LP, 1, T + 16 * s2 * LP + 16 * b, 1, LP, true);
+        st16(T + 16 * r * LP + 16 * s2, acc, 1.0);
+      };
+      if (w == 0) upd(b + 1, b + 1);
+      int idx = 0;
+      for (int r = b + 1; r <= 3; ++r)
+        for (int s2 = b + 1; s2 <= r; ++s2) {
+          if (r == b + 1 && s2 == b + 1) continue;
+          if (w >= 1 && idx % 3 == w - 1) upd(r, s2);
+          ++idx;
+        }
+    }
+  });
+  // inverse: wave c builds column block c (X_cc = Dinv_c already in U); scratch = T's upper
+  // block (c, r)
+  if (w < 3) {
+    const int c = w;
+    for (int r = c + 1; r <= 3; ++r) {
+      f64x4 acc = zero4();
+      for (int k = c; k < r; ++k)
+        mm16(acc, T + 16 * r * LP + 16 * k, LP, 1, U + 16 * k * LP + 16 * c, LP, 1, false);
+      lds_double* tmp = T + 16 * c * LP + 16 * r;
+      st16(tmp, acc, 1.0);
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the block is in LDS before it is read
+      f64x4 x = zero4();
+      mm16(x, U + 16 * r * LP + 16 * r, LP, 1, tmp, LP, 1, false);
+      st16(U + 16 * r * LP + 16 * c, x, -1.0);
+    }
+  }
+  __syncthreads();
+  // zero the strict upper blocks of L and L^-1
+  for (int g = threadIdx.x; g < NB * NB; g += 256) {
+    const int r = g >> 6, cc = g & 63;
+    if ((cc >> 4) > (r >> 4)) {
+      T[r * LP + cc] = 0.0;
+      U[r * LP + cc] = 0.0;
+    }
+  }
+  if (threadIdx.x == 0) {
+    sm.fail = fail;
+    sm.red[0] = lg;
+  }
+  __syncthreads();
+  const int f = sm.fail;
+  if (ld_out) *ld_out = sm.red[0];
+  __syncthreads();
+  return f;
+}
+
 // Factor diagonal block k whose (updated, symmetric) tile is in sm.As as [row][col]; write
 // L_kk into A, D_k into X (dk_ptr), accumulate logdet, set info.
 template <int MODE>
@@ -321,7 +484,7 @@ GP_DEV void diag_block(Smem& sm, double* __restrict__ Ab, int lda, double* __res
                        int ldx, int n, int k, int* info, double* logdet, int b) {
   const int k0 = k * NB, nb = min(NB, n - k0);
   double lg = 0.0;
-  const int f = diag_factor_inv(nb, &lg);
+  const int f = diag_factor_inv<0>(nb, &lg);
   if (f) {
     if (threadIdx.x == 0 && info) info[b] = k0 + f;
     return;
@@ -687,6 +850,673 @@ __global__ void trtri_info_kernel(int* __restrict__ info, int batch) {
   if (b < batch && info[b] == 0x7f7f7f7f) info[b] = 0;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Persistent dataflow factorisation (gp_potrf_inv / gp_potrf for N = ceil(n/64) <= kPPMaxN).
+//
+// One launch replaces the 2N launches of potrf_sweep.  Left-looking on 64x64 tiles: every
+// tile is finished by ONE workgroup that keeps its 64x64 accumulator in registers across all
+// of its K steps (the trailing matrix is never re-read / re-written per step as in the
+// right-looking sweep), and workgroups hand tiles to each other through per-tile flags.
+//   chain (one workgroup per problem, for j = 0..N-1):
+//     C_jj = P_jj - L_j,j-1 L_j,j-1^T ; (L_jj, D_j = L_jj^-1) = diag_factor_inv(C_jj) ;
+//     L_j+1,j = P_j+1,j D_j^T  (kept in LDS for the next step's SYRK)
+//   worker tasks, dequeued in one global order (schedule_kernel):
+//     DP(j)  P_jj    = A_jj    - sum_{k<j-1} L_jk L_jk^T      (in place in A, for the chain)
+//     SP(j)  P_j+1,j = A_j+1,j - sum_{k<j}   L_j+1,k L_jk^T   (in place in A, for the chain)
+//     LT(i,j), i >= j+2:  L_ij = (A_ij - sum_{k<j} L_ik L_jk^T) D_j^T
+//     XT(i,c), i > c:     X_ic = -D_i sum_{k=c}^{i-1} L_ik X_kc   (X = L^-1, X_cc = D_c)
+// The dequeue order is topological (every task's inputs come from tasks earlier in the list,
+// or from the chain, which only waits on DP/SP tasks that precede everything waiting on it),
+// so the launch is deadlock-free for any residency; anti-diagonal keys put the tiles the
+// chain needs next at the front.
+// Hand-offs follow MI355X_MICROARCH.md's acquire-free form: produced tiles are stored with
+// sc1 (write-through) 16-B stores, each storing wave waits vmcnt(0), the workgroup barriers,
+// one lane stores the flag (sc1); consumers poll flags with sc1 loads and read every produced
+// byte with sc1 loads.  Every wait also watches the problem's abort word (non-PD pivot) and a
+// poll budget, so no path can spin forever.
+// ------------------------------------------------------------------------------------------
+constexpr int kPPMaxN = 250;          // schedule_kernel: one thread per key (4N+23 <= 1024)
+constexpr int kTChain = 0, kTL = 1, kTDP = 2, kTSP = 3, kTX = 4;
+constexpr long long kPollBudget = 1ll << 22;   // s_sleep polls before a wait gives up
+
+__shared__ double g_keep[NB * LP];    // chain: L_j+1,j as [p][r] (opA layout) between steps
+__shared__ int g_msg[4];              // dequeued task / wait results broadcast to the workgroup
+
+struct PPArgs {
+  double* A; long long sA; int lda;
+  double* X; long long sX; int ldx;   // L^-1 (inv) or the 64 x 64N D_k scratch (plain)
+  int n, N, batch, inv;
+  int* info; double* logdet;
+  const int2* tasks; int ntasks;
+  int* head;
+  int* flags; int fstride;            // per problem: FL[N*N], FX[N*N], DPF[N], SPF[N], abort
+  int* dbg;                           // debug only: per-workgroup progress words (host memory)
+  long long* trace;                   // debug only: per-task / per-chain-step timestamps
+};
+
+GP_DEV long long pp_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+#define PP_TRACE(P, idx, val)                                                            \
+  do {                                                                                   \
+    if ((P).trace && threadIdx.x == 0) (P).trace[(idx)] = (val);                         \
+  } while (0)
+
+#define PP_MARK(P, code, val)                                                            \
+  do {                                                                                   \
+    if ((P).dbg && threadIdx.x == 0) {                                                   \
+      __hip_atomic_store((P).dbg + blockIdx.x * 4 + 1, (code), __ATOMIC_RELAXED,         \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                     \
+      __hip_atomic_store((P).dbg + blockIdx.x * 4 + 2, (val), __ATOMIC_RELAXED,          \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                     \
+    }                                                                                    \
+  } while (0)
+
+GP_DEV __amdgpu_buffer_rsrc_t pp_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+GP_DEV int pp_ldflag(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+GP_DEV void pp_stflag(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+typedef unsigned int pp_u4 __attribute__((ext_vector_type(4)));
+
+// Tile load into registers (load_op's slot map) with sc1 loads: 16-B buffer loads for a full,
+// aligned tile, else bounds-checked 8-B loads (zero outside fv x sv).
+GP_DEV void pp_load(OpTile& t, const double* src, int ld, int fv, int sv) {
+  const int tid = threadIdx.x;
+  const bool full = fv == NB && sv == NB && (ld & 1) == 0 && (((size_t)src & 15) == 0);
+  if (full) {
+    const __amdgpu_buffer_rsrc_t r = pp_rsrc(src);
+    const int base = ((tid & 31) * 2 + (tid >> 5) * ld) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const pp_u4 x = __builtin_amdgcn_raw_buffer_load_b128(r, base + q * 64 * ld, 0, 16);
+      t.v[2 * q] = __longlong_as_double(((long long)x.y << 32) | x.x);
+      t.v[2 * q + 1] = __longlong_as_double(((long long)x.w << 32) | x.z);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int g = tid + 256 * q;
+      const int f = (g & 31) * 2, sl = g >> 5;
+      const double* p = src + f + (long long)sl * ld;
+      const bool ok = sl < sv;
+      t.v[2 * q] = (ok && f < fv)
+          ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+      t.v[2 * q + 1] = (ok && f + 1 < fv)
+          ? __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    }
+  }
+}
+
+// Store a tile held in LDS as Cs[col][row] (pitch LP) to dst (col-major, ld) with sc1 stores,
+// rows < rv and cols < cv only (and row >= col with `lower`); `neg` stores -Cs.
+GP_DEV void pp_store_cm(double* dst, int ld, const double* Cs, int rv, int cv, bool neg,
+                        bool lower = false) {
+  const int tid = threadIdx.x;
+  const double sg = neg ? -1.0 : 1.0;
+  const bool full = rv == NB && cv == NB && !lower && (ld & 1) == 0 &&
+                    (((size_t)dst & 15) == 0);
+  if (full) {
+    const __amdgpu_buffer_rsrc_t r = pp_rsrc(dst);
+    const int f = (tid & 31) * 2;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int sl = (tid >> 5) + 8 * q;
+      const double a = sg * Cs[sl * LP + f], b = sg * Cs[sl * LP + f + 1];
+      const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+      pp_u4 x;
+      x.x = (unsigned)ua; x.y = (unsigned)(ua >> 32); x.z = (unsigned)ub; x.w = (unsigned)(ub >> 32);
+      __builtin_amdgcn_raw_buffer_store_b128(x, r, (f + sl * ld) * 8, 0, 16);
+    }
+  } else {
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      int row, col;
+      slot_rc(q, row, col);
+      if (row < rv && col < cv && (!lower || row >= col))
+        __hip_atomic_store(dst + row + (long long)col * ld, sg * Cs[col * LP + row],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Store the nb x nb tile held in LDS as T[row][col] (pitch LP) to dst (col-major, ld) with sc1
+// stores: 16-B pairs of rows for a full aligned tile, else 8-B elements; `lower`: only
+// row >= col (LAPACK: the strict upper triangle of A is never written).
+GP_DEV void pp_store_rm(double* dst, int ld, const double* T, int nb, bool lower) {
+  const int tid = threadIdx.x;
+  const bool full = nb == NB && (ld & 1) == 0 && (((size_t)dst & 15) == 0);
+  if (full) {
+    const __amdgpu_buffer_rsrc_t r = pp_rsrc(dst);
+    const int f = (tid & 31) * 2;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = (tid >> 5) + 8 * q;
+      const double a = T[f * LP + c], b = T[(f + 1) * LP + c];
+      if (!lower || f >= c) {
+        const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+        pp_u4 x;
+        x.x = (unsigned)ua; x.y = (unsigned)(ua >> 32); x.z = (unsigned)ub; x.w = (unsigned)(ub >> 32);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, (f + c * ld) * 8, 0, 16);
+      } else if (f + 1 == c) {
+        __hip_atomic_store(dst + c + (long long)c * ld, b, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else {
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      int row, col;
+      slot_rc(q, row, col);
+      if (row < nb && col < nb && (!lower || row >= col))
+        __hip_atomic_store(dst + row + (long long)col * ld, T[row * LP + col], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Every storing wave drains its stores, then one lane raises the flag.
+GP_DEV void pp_publish(int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) pp_stflag(flag, 1);
+}
+
+// acc (this wave's 32x32) += sum_k As[k][rows] * Bs[k][cols]   (mma64 without the zeroing)
+GP_DEV void mma64_add(const double* As, const double* Bs, f64x4 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
+#pragma unroll 4
+  for (int k4 = 0; k4 < NB / 4; ++k4) {
+    const int k = k4 + (NB / 4) * lk;
+    const double a0 = As[k * LP + wr * 32 + li], a1 = As[k * LP + wr * 32 + 16 + li];
+    const double b0 = Bs[k * LP + wc * 32 + li], b1 = Bs[k * LP + wc * 32 + 16 + li];
+    acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
+    acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
+    acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
+    acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+  }
+}
+
+// The block's accumulator into LDS row-major: Cs[row][col] (pitch LP).
+GP_DEV void acc_to_lds_rm(double* Cs, const f64x4 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + mi * 16 + lk + 4 * r, col = wc * 32 + nj * 16 + li;
+        Cs[row * LP + col] = acc[mi][nj][r];
+      }
+}
+
+// Wait until the flag *f is set, or the problem aborted / the poll budget ran out (then
+// false).  One lane polls; the verdict is broadcast through g_msg (all threads call).
+GP_DEV bool pp_wait1(const int* f, int* abort) {
+  if (threadIdx.x == 0) {
+    int ok = 0;
+    for (long long it = 0; it < kPollBudget; ++it) {
+      if (pp_ldflag(f)) { ok = 1; break; }
+      if (pp_ldflag(abort)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok && !pp_ldflag(abort)) pp_stflag(abort, 2);   // budget spent: give up the problem
+    g_msg[1] = ok;
+  }
+  __syncthreads();
+  const int ok = g_msg[1];
+  __syncthreads();
+  return ok != 0;
+}
+
+// One K step of a worker task: opA tile (NAT), opB tile (NAT or TRN), the two producer flags.
+struct PPTerm {
+  const double *a, *b;
+  const int *fa, *fb;
+  int lda_, ldb_, av, bv;   // av: valid rows of opA's tile; bv: valid rows of opB's (NAT)
+  bool btrn;
+};
+
+struct PPTask {
+  int kind, b, i, j, nterms, idx;
+};
+
+GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
+  const int N = P.N;
+  double* Ab = P.A + T.b * P.sA;
+  double* Xb = P.X + T.b * P.sX;
+  const int* F = P.flags + (long long)T.b * P.fstride;
+  auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
+  auto rv = [&](int r) { return min(NB, P.n - r * NB); };
+  PPTerm u;
+  u.lda_ = P.lda;
+  u.ldb_ = P.lda;
+  u.btrn = false;
+  if (T.kind == kTL || T.kind == kTSP) {   // L_ik L_jk^T with (i, j) = (T.i, T.j)
+    u.a = atile(T.i, t);  u.fa = F + T.i * N + t;  u.av = rv(T.i);
+    u.b = atile(T.j, t);  u.fb = F + T.j * N + t;  u.bv = rv(T.j);
+  } else if (T.kind == kTDP) {             // L_jk L_jk^T
+    u.a = atile(T.j, t);  u.fa = F + T.j * N + t;  u.av = rv(T.j);
+    u.b = u.a;            u.fb = u.fa;             u.bv = u.av;
+  } else {                                 // XT: L_ik X_kc, k = c + t (X_cc = D_c)
+    const int k = T.j + t;
+    u.a = atile(T.i, k);  u.fa = F + T.i * N + k;  u.av = rv(T.i);
+    u.b = Xb + k * NB + (long long)T.j * NB * P.ldx;
+    u.ldb_ = P.ldx;
+    u.fb = (k == T.j) ? F + k * N + k : F + N * N + k * N + T.j;
+    u.bv = NB;                               // X is zero-padded to npad: always in bounds
+    u.btrn = true;
+  }
+  return u;
+}
+
+// Lane-parallel readiness scan: the number of consecutive terms t0, t0+1, ... whose two input
+// flags are set (wave 0, one term per lane), at least 1 unless the problem aborted (-1).
+GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int res = -1;
+    for (long long it = 0; it < kPollBudget; ++it) {
+      const int t = t0 + lane;
+      bool rdy = true;
+      if (t < T.nterms) {
+        const PPTerm u = pp_term(P, T, t);
+        rdy = pp_ldflag(u.fa) != 0 && pp_ldflag(u.fb) != 0;
+      }
+      const unsigned long long m = __ballot(rdy);
+      const int lead = (~m == 0ull) ? 64 : __builtin_ctzll(~m);
+      const int cnt = min(lead, T.nterms - t0);
+      if (cnt > 0) { res = cnt; break; }
+      if (pp_ldflag(abort)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (res < 0 && lane == 0 && !pp_ldflag(abort)) pp_stflag(abort, 2);
+    if (lane == 0) g_msg[2] = res;
+  }
+  __syncthreads();
+  const int r = g_msg[2];
+  __syncthreads();
+  return r;
+}
+
+GP_DEV void pp_load_term(const PPTerm& u, OpTile& ta, OpTile& tb) {
+  pp_load(ta, u.a, u.lda_, u.av, NB);
+  if (u.b != u.a) pp_load(tb, u.b, u.ldb_, u.bv, NB);
+}
+
+// Worker: accumulate the task's K steps in registers (software-pipelined: the next step's
+// operands are loaded while the current step's MFMAs run, whenever its flags are known set).
+GP_DEV bool pp_accumulate(const PPArgs& P, const PPTask& T, f64x4 (&acc)[2][2], int* abort) {
+  Smem& sm = g_sm;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = zero4();
+  if (T.nterms == 0) return true;
+  OpTile ta, tb;
+  int avail = pp_ready(P, T, 0, abort);      // terms [0, avail) are ready
+  if (avail < 0) return false;
+  PPTerm u = pp_term(P, T, 0);
+  pp_load_term(u, ta, tb);
+  for (int t = 0; t < T.nterms; ++t) {
+    const bool same = u.b == u.a;
+    const bool trn = u.btrn;
+    __syncthreads();                                   // the previous MFMAs have read As / Bs
+    store_op<false>(sm.As, ta);
+    if (!same) {
+      if (trn) store_op<true>(sm.Bs, tb);
+      else store_op<false>(sm.Bs, tb);
+    }
+    __syncthreads();
+    const bool more = t + 1 < T.nterms;
+    const bool pre = more && t + 1 < avail;
+    if (pre) {
+      u = pp_term(P, T, t + 1);
+      pp_load_term(u, ta, tb);
+    }
+    mma64_add(sm.As, same ? sm.As : sm.Bs, acc);
+    if (more && !pre) {
+      const int r = pp_ready(P, T, t + 1, abort);
+      if (r < 0) return false;
+      avail = t + 1 + r;
+      u = pp_term(P, T, t + 1);
+      pp_load_term(u, ta, tb);
+    }
+  }
+  return true;
+}
+
+// C (As as [col][row]) = A tile - acc, for rows < rv / cols < cv (zero elsewhere).  lower:
+// only row >= col is read from A (diagonal tiles; the upper part of A is never read).
+GP_DEV void pp_sub_from_a(const double* src, int ld, int rv, int cv, bool lower,
+                          const f64x4 (&acc)[2][2]) {
+  Smem& sm = g_sm;
+  __syncthreads();
+  acc_to_lds(sm.As, acc);
+  __syncthreads();
+#pragma unroll 4
+  for (int q = 0; q < 16; ++q) {
+    int row, col;
+    slot_rc(q, row, col);
+    const bool ok = row < rv && col < cv && (!lower || row >= col);
+    const double a = ok ? __hip_atomic_load(src + row + (long long)col * ld, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    sm.As[col * LP + row] = ok ? a - sm.As[col * LP + row] : 0.0;
+  }
+  __syncthreads();
+}
+
+GP_DEV double* pp_dptr(const PPArgs& P, int b, int j, int& ld) {
+  double* Xb = P.X + b * P.sX;
+  if (P.inv) {
+    ld = P.ldx;
+    return Xb + j * NB + (long long)j * NB * P.ldx;
+  }
+  ld = NB;
+  return Xb + (long long)j * NB * NB;
+}
+
+GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
+  Smem& sm = g_sm;
+  const int N = P.N;
+  int* F = P.flags + (long long)T.b * P.fstride;
+  int* abort = F + 2 * N * N + 2 * N;
+  if (pp_ldflag(abort)) return;
+  double* Ab = P.A + T.b * P.sA;
+  f64x4 acc[2][2];
+  PP_MARK(P, 20 + T.kind, T.i * 1000 + T.j);
+  PP_TRACE(P, (long long)T.idx * 4 + 0, blockIdx.x);
+  PP_TRACE(P, (long long)T.idx * 4 + 1, pp_now());
+  if (!pp_accumulate(P, T, acc, abort)) return;
+  PP_MARK(P, 30 + T.kind, T.i * 1000 + T.j);
+  PP_TRACE(P, (long long)T.idx * 4 + 2, pp_now());
+  auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
+  auto rv = [&](int r) { return min(NB, P.n - r * NB); };
+  if (T.kind == kTDP || T.kind == kTSP) {
+    // partial sums for the chain, in place in A
+    const int r = T.kind == kTDP ? T.j : T.j + 1;
+    double* dst = atile(r, T.j);
+    pp_sub_from_a(dst, P.lda, rv(r), rv(T.j), T.kind == kTDP, acc);
+    pp_store_cm(dst, P.lda, sm.As, rv(r), rv(T.j), false, T.kind == kTDP);
+    pp_publish(T.kind == kTDP ? F + 2 * N * N + T.j : F + 2 * N * N + N + T.j);
+    PP_TRACE(P, (long long)T.idx * 4 + 3, pp_now());
+    return;
+  }
+  if (T.kind == kTL) {
+    // L_ij = (A_ij - acc) D_j^T
+    double* dst = atile(T.i, T.j);
+    pp_sub_from_a(dst, P.lda, rv(T.i), NB, false, acc);
+    if (!pp_wait1(F + T.j * N + T.j, abort)) return;
+    int ldd;
+    const double* D = pp_dptr(P, T.b, T.j, ldd);
+    OpTile td;
+    pp_load(td, D, ldd, NB, NB);                        // Bs[p][c] = D_j[c][p]
+    store_op<false>(sm.Bs, td);
+    __syncthreads();
+    mma64(sm.As, sm.Bs, acc);
+    __syncthreads();
+    acc_to_lds(sm.As, acc);
+    __syncthreads();
+    pp_store_cm(dst, P.lda, sm.As, rv(T.i), NB, false);
+    pp_publish(F + T.i * N + T.j);
+    PP_TRACE(P, (long long)T.idx * 4 + 3, pp_now());
+    return;
+  }
+  // XT: X_ic = -D_i S, S = acc
+  __syncthreads();
+  acc_to_lds_rm(sm.Bs, acc);                            // Bs[p][cc] = S[p][cc]
+  if (!pp_wait1(F + T.i * N + T.i, abort)) return;
+  PP_MARK(P, 40, T.i * 1000 + T.j);
+  int ldd;
+  const double* D = pp_dptr(P, T.b, T.i, ldd);
+  OpTile td;
+  pp_load(td, D, ldd, NB, NB);                          // As[p][r] = D_i[r][p]
+  store_op<false>(sm.As, td);
+  __syncthreads();
+  mma64(sm.As, sm.Bs, acc);
+  __syncthreads();
+  acc_to_lds(sm.As, acc);
+  __syncthreads();
+  double* Xb = P.X + T.b * P.sX;
+  pp_store_cm(Xb + T.i * NB + (long long)T.j * NB * P.ldx, P.ldx, sm.As, NB, NB, true);
+  pp_publish(F + N * N + T.i * N + T.j);
+  PP_MARK(P, 41, T.i * 1000 + T.j);
+  PP_TRACE(P, (long long)T.idx * 4 + 3, pp_now());
+}
+
+// The chain of problem b (see the section comment).
+GP_DEV void pp_chain(const PPArgs& P, int b) {
+  Smem& sm = g_sm;
+  const int N = P.N;
+  int* F = P.flags + (long long)b * P.fstride;
+  int* abort = F + 2 * N * N + 2 * N;
+  double* Ab = P.A + b * P.sA;
+  auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
+  double ld_sum = 0.0;
+  for (int j = 0; j < N; ++j) {
+    const int nb = min(NB, P.n - j * NB);
+    PP_MARK(P, 10, j);
+    const long long tb0 = (long long)P.ntasks * 4 + ((long long)b * N + j) * 8;
+    PP_TRACE(P, tb0 + 0, pp_now());
+    // (a) C_jj = P_jj - L_j,j-1 L_j,j-1^T into As as a full symmetric [row][col] tile.  The
+    // P_jj loads (16-B sc1, the whole tile; only its lower triangle is used) are in flight
+    // during the SYRK.
+    if (j >= 2 && !pp_wait1(F + 2 * N * N + j, abort)) return;
+    PP_TRACE(P, tb0 + 1, pp_now());
+    OpTile tpj;
+    pp_load(tpj, atile(j, j), P.lda, nb, nb);
+    f64x4 acc[2][2];
+    if (j >= 1) mma64(g_keep, g_keep, acc);
+    else {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = zero4();
+    }
+    __syncthreads();
+    acc_to_lds(sm.Bs, acc);                             // Bs[col][row] = acc(row, col)
+    store_op<false>(sm.As, tpj);                        // As[c][r] = P(r, c) (r >= c valid)
+    __syncthreads();
+    for (int g = threadIdx.x; g < NB * NB; g += 256) {
+      const int r = g & (NB - 1), c = g >> 6;           // lower element (r, c), r >= c
+      if (r < c) continue;
+      double v;
+      if (r < nb) v = sm.As[c * LP + r] - sm.Bs[c * LP + r];
+      else v = (r == c) ? 1.0 : 0.0;
+      sm.As[r * LP + c] = v;
+      sm.As[c * LP + r] = v;
+    }
+    __syncthreads();
+    // (b) factor + invert
+    PP_MARK(P, 11, j);
+    PP_TRACE(P, tb0 + 2, pp_now());
+    double lg = 0.0;
+    const int f = diag_factor_blk(nb, &lg);
+    PP_TRACE(P, tb0 + 3, pp_now());
+    if (f) {
+      if (threadIdx.x == 0) {
+        if (P.info) P.info[b] = j * NB + f;
+        pp_stflag(abort, 1);
+      }
+      return;
+    }
+    ld_sum += lg;
+    PP_MARK(P, 12, j);
+    // L_jj -> A (lower, LAPACK layout), D_j -> X_jj (or the D scratch); sm.As / sm.Bs hold
+    // them as [row][col]
+    {
+      int ldd;
+      double* D = pp_dptr(P, b, j, ldd);
+      pp_store_rm(D, ldd, sm.Bs, nb, false);
+    }
+    pp_publish(F + j * N + j);
+    pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);   // L_jj: read by nobody in this launch
+    PP_TRACE(P, tb0 + 4, pp_now());
+    if (j + 1 >= N) break;
+    // (c) L_j+1,j = P_j+1,j D_j^T
+    PP_MARK(P, 13, j);
+    const int nb1 = min(NB, P.n - (j + 1) * NB);
+    if (j >= 1 && !pp_wait1(F + 2 * N * N + N + j, abort)) return;
+    PP_TRACE(P, tb0 + 5, pp_now());
+    OpTile tp;
+    pp_load(tp, atile(j + 1, j), P.lda, nb1, NB);      // As[p][r] = P[r][p]
+    // D_j^T: Bs[p][c] = D[c][p] from Bs[row][col] = D[row][col] (in-place transpose)
+    for (int g = threadIdx.x; g < NB * NB; g += 256) {
+      const int r = g & (NB - 1), c = g >> 6;
+      if (r > c) {
+        const double x = sm.Bs[r * LP + c], y = sm.Bs[c * LP + r];
+        sm.Bs[r * LP + c] = y;
+        sm.Bs[c * LP + r] = x;
+      }
+    }
+    __syncthreads();
+    store_op<false>(sm.As, tp);
+    __syncthreads();
+    PP_MARK(P, 14, j);
+    PP_TRACE(P, tb0 + 6, pp_now());
+    mma64(sm.As, sm.Bs, acc);
+    __syncthreads();
+    acc_to_lds(g_keep, acc);                           // keep[c][r] = L_j+1,j(r, c)
+    __syncthreads();
+    pp_store_cm(atile(j + 1, j), P.lda, g_keep, nb1, NB, false);
+    pp_publish(F + (j + 1) * N + j);
+    PP_MARK(P, 15, j);
+    PP_TRACE(P, tb0 + 7, pp_now());
+  }
+  if (threadIdx.x == 0 && P.logdet) P.logdet[b] = ld_sum;
+}
+
+// Chain wrapper: a poll budget spent anywhere in problem b (abort word 2) is reported as
+// info[b] = -1 (an internal error, never a pivot).
+GP_DEV void pp_chain_run(const PPArgs& P, int b) {
+  pp_chain(P, b);
+  if (threadIdx.x == 0) {
+    int* abort = P.flags + (long long)b * P.fstride + 2 * P.N * P.N + 2 * P.N;
+    if (pp_ldflag(abort) == 2 && P.info) P.info[b] = -1;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
+  for (;;) {
+    if (threadIdx.x == 0) g_msg[0] = atomicAdd(P.head, 1);
+    __syncthreads();
+    const int t = g_msg[0];
+    __syncthreads();
+    if (P.dbg && threadIdx.x == 0)
+      __hip_atomic_store(P.dbg + blockIdx.x * 4, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t >= P.ntasks) { PP_MARK(P, 99, 0); return; }
+    const int2 e = P.tasks[t];
+    PPTask T;
+    T.kind = e.x & 15;
+    T.b = e.x >> 4;
+    T.i = e.y & 0xffff;
+    T.j = e.y >> 16;
+    if (T.kind == kTChain) {
+      pp_chain_run(P, T.b);
+      continue;
+    }
+    T.idx = t;
+    T.nterms = T.kind == kTL ? T.j : T.kind == kTDP ? T.j - 1 : T.kind == kTSP ? T.j : T.i - T.j;
+    pp_worker(P, T);
+  }
+}
+
+// Task list: batch chain entries, then per key t = 0..4N-2+4W (anti-diagonal order, see the
+// section comment) the tasks of that key, each for every problem:
+//   DP(j): t = 4j-2;  SP(j): t = 4j+1;  band LT(i,j), i-j <= kPPBand: t = 2(i+j)   ("early")
+//   other LT(i,j): t = 2(i+j) + 4W;  XT(i,c): t = 4i+2 + 4W
+// The early tasks are what the chain waits on (its partials and the near-diagonal tiles the
+// partials wait on): they are dequeued kPPLead = W chain steps ahead of their topological
+// position, early enough to catch up on their K steps that are already available.  Only
+// early tasks can wait on tasks not yet dequeued, and at most ~W (2 + kPPBand) of them wait at
+// a time, far fewer than the workers, so the order stays deadlock-free.
+constexpr int kPPLead = 6;
+constexpr int kPPBand = 3;
+
+// LT tiles (s - j, j) on anti-diagonal s with band (i - j <= kPPBand) or not: j range.
+GP_DEV void pp_lt_range(int s, int N, bool band, int& jmin, int& jmax) {
+  jmin = max(0, s - (N - 1));
+  if (band) {
+    jmin = max(jmin, (s - kPPBand + 1) / 2);   // s - 2j <= kPPBand
+    jmax = (s - 2) / 2;                         // s - 2j >= 2
+  } else {
+    jmax = s >= kPPBand + 1 ? (s - kPPBand - 1) / 2 : -1;   // s - 2j >= kPPBand + 1
+  }
+  if (s < 2) jmax = -1;
+}
+
+__device__ int pp_key_count(int t, int N, bool inv) {
+  int c = 0, jmin, jmax;
+  if (t % 4 == 2 && (t + 2) / 4 >= 2 && (t + 2) / 4 <= N - 1) ++c;            // DP
+  if (t % 4 == 1 && (t - 1) / 4 >= 1 && (t - 1) / 4 <= N - 2) ++c;            // SP
+  if (t % 2 == 0) {                                                            // band LT
+    pp_lt_range(t / 2, N, true, jmin, jmax);
+    c += max(0, jmax - jmin + 1);
+  }
+  const int K = t - 4 * kPPLead;
+  if (K < 0) return c;
+  if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) c += (K - 2) / 4;  // XT
+  if (K % 2 == 0) {                                                            // other LT
+    pp_lt_range(K / 2, N, false, jmin, jmax);
+    c += max(0, jmax - jmin + 1);
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, int batch,
+                                                           int inv) {
+  __shared__ int cnt[2][1024];
+  const int T = threadIdx.x;
+  const int nk = 4 * N - 1 + 4 * kPPLead;
+  const int own = T < nk ? pp_key_count(T, N, inv != 0) : 0;
+  cnt[0][T] = own;
+  __syncthreads();
+  int src = 0;
+  for (int off = 1; off < 1024; off <<= 1) {   // inclusive Hillis-Steele scan
+    cnt[src ^ 1][T] = cnt[src][T] + (T >= off ? cnt[src][T - off] : 0);
+    __syncthreads();
+    src ^= 1;
+  }
+  for (int b = T; b < batch; b += blockDim.x) tasks[b] = make_int2(kTChain | (b << 4), 0);
+  if (T >= nk) return;
+  const int excl = cnt[src][T] - own;
+  long long pos = batch + (long long)excl * batch;
+  auto emit = [&](int kind, int i, int j) {
+    for (int b = 0; b < batch; ++b) tasks[pos++] = make_int2(kind | (b << 4), i | (j << 16));
+  };
+  int jmin, jmax;
+  if (T % 4 == 2 && (T + 2) / 4 >= 2 && (T + 2) / 4 <= N - 1) emit(kTDP, 0, (T + 2) / 4);
+  if (T % 4 == 1 && (T - 1) / 4 >= 1 && (T - 1) / 4 <= N - 2) emit(kTSP, (T - 1) / 4 + 1, (T - 1) / 4);
+  if (T % 2 == 0) {
+    pp_lt_range(T / 2, N, true, jmin, jmax);
+    for (int j = jmax; j >= jmin; --j) emit(kTL, T / 2 - j, j);
+  }
+  const int K = T - 4 * kPPLead;
+  if (K < 0) return;
+  if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) {
+    const int i = (K - 2) / 4;
+    for (int c = i - 1; c >= 0; --c) emit(kTX, i, c);   // nearest the diagonal first
+  }
+  if (K % 2 == 0) {
+    pp_lt_range(K / 2, N, false, jmin, jmax);
+    for (int j = jmax; j >= jmin; --j) emit(kTL, K / 2 - j, j);
+  }
+}
+
+long long pp_task_count(int N, bool inv) {
+  const long long lt = (long long)(N - 1) * (N - 2) / 2;
+  const long long dp = N >= 3 ? N - 2 : 0, sp = N >= 3 ? N - 2 : 0;
+  const long long xt = inv ? (long long)N * (N - 1) / 2 : 0;
+  return 1 + lt + dp + sp + xt;
+}
+
 }  // namespace
 
 static_assert(GPFIT_POTRF_NB == NB, "gpfit_internal.h must match the blocking");
@@ -740,6 +1570,62 @@ static int potrf_sweep(double* A, int n, int lda, long long sA, double* X, int l
   return 0;
 }
 
+static int num_cus() {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    return n;
+  }();
+  return ncu;
+}
+
+// The persistent dataflow factorisation (pp_kernel) on `stream`: stream-ordered scratch for the
+// task list, the dequeue head and the per-tile flags (hipMallocAsync / hipFreeAsync), one
+// schedule launch, one persistent launch with one workgroup per CU.  X is L^-1 (inv, zeroed by
+// the caller) or the 64 x 64N D_k scratch (ldx = 64).
+static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx, long long sX,
+                     int batch, int* info, double* logdet, bool inv, hipStream_t stream) {
+  const int N = gp_ceil_div(n, NB);
+  const long long ntasks = pp_task_count(N, inv) * batch;
+  const int fstride = ((2 * N * N + 2 * N + 1 + 31) / 32) * 32;
+  const size_t task_bytes = ((size_t)ntasks * sizeof(int2) + 255) / 256 * 256;
+  const size_t flag_bytes = 256 + (size_t)batch * fstride * sizeof(int);
+  char* scr = nullptr;
+  GP_CK(hipMallocAsync(reinterpret_cast<void**>(&scr), task_bytes + flag_bytes, stream));
+  GP_CK(hipMemsetAsync(scr + task_bytes, 0, flag_bytes, stream));
+  int2* tasks = reinterpret_cast<int2*>(scr);
+  int* head = reinterpret_cast<int*>(scr + task_bytes);
+  int* flags = reinterpret_cast<int*>(scr + task_bytes + 256);
+  hipLaunchKernelGGL(pp_schedule_kernel, dim3(1), dim3(1024), 0, stream, tasks, N, batch,
+                     inv ? 1 : 0);
+  GP_CK(hipGetLastError());
+  PPArgs P;
+  P.A = A; P.sA = sA; P.lda = lda;
+  P.X = X; P.sX = sX; P.ldx = ldx;
+  P.n = n; P.N = N; P.batch = batch; P.inv = inv ? 1 : 0;
+  P.info = info; P.logdet = logdet;
+  P.tasks = tasks; P.ntasks = (int)ntasks;
+  P.head = head; P.flags = flags; P.fstride = fstride;
+  const char* dbg = std::getenv("GPFIT_PP_DEBUG_PTR");   // debug only: pinned host int[4*#CU]
+  P.dbg = dbg ? reinterpret_cast<int*>(std::strtoull(dbg, nullptr, 0)) : nullptr;
+  const char* trc = std::getenv("GPFIT_PP_TRACE_PTR");   // debug only: device int64 buffer
+  P.trace = trc ? reinterpret_cast<long long*>(std::strtoull(trc, nullptr, 0)) : nullptr;
+  const int grid = (int)(ntasks < num_cus() ? ntasks : num_cus());
+  hipLaunchKernelGGL(pp_kernel, dim3(grid), dim3(256), 0, stream, P);
+  GP_CK(hipGetLastError());
+  GP_CK(hipFreeAsync(scr, stream));
+  return 0;
+}
+
+static bool pp_eligible(int n, int batch) {
+  const int N = gp_ceil_div(n, NB);
+  return N <= kPPMaxN && pp_task_count(N, true) * (long long)batch < (1ll << 30) &&
+         std::getenv("GPFIT_POTRF_SWEEP") == nullptr;
+}
+
 // Zero L^-1 (upper triangle + padding): one memset for a packed batch, else one 2-D memset per
 // problem.
 static hipError_t zero_linv(double* Linv, int npad, int ldinv, long long strideInv, int batch,
@@ -779,8 +1665,14 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
   if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
   GP_CK(zero_linv(Linv, npad, ldinv, strideInv, batch, stream));
   gpfit_prof_begin(GP_PROF_POTRF, stream);
-  const int rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info,
-                                        logdet, stream, k_ev, ev);
+  int rc;
+  if (pp_eligible(n, batch)) {
+    rc = pp_factor(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet, true, stream);
+    if (rc == 0 && ev) GP_CK(hipEventRecord(ev, stream));
+  } else {
+    rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,
+                                stream, k_ev, ev);
+  }
   gpfit_prof_end(GP_PROF_POTRF, stream);
   return rc;
 }
@@ -800,8 +1692,10 @@ extern "C" int gp_potrf(double* A, int n, int lda, long long strideA, int batch,
   const long long sD = (long long)NB * N * NB;
   double* D = nullptr;
   GP_CK(hipMallocAsync(reinterpret_cast<void**>(&D), sizeof(double) * sD * batch, stream));
-  const int rc = potrf_sweep<kPotrf>(A, n, lda, strideA, D, NB, sD, batch, info, logdet, stream,
-                                     -1, nullptr);
+  const int rc = pp_eligible(n, batch)
+      ? pp_factor(A, n, lda, strideA, D, NB, sD, batch, info, logdet, false, stream)
+      : potrf_sweep<kPotrf>(A, n, lda, strideA, D, NB, sD, batch, info, logdet, stream, -1,
+                            nullptr);
   GP_CK(hipFreeAsync(D, stream));
   return rc;
 }
