@@ -171,6 +171,10 @@ def main():
     ap.add_argument("--serial", action="store_true",
                     help="c3: no context; gram, potrf, cross-covariance, predict in order on "
                          "one stream")
+    ap.add_argument("--cross-start", type=float, default=-1.0,
+                    help="c3: gp_ctx cross_start (-1: library default)")
+    ap.add_argument("--aux-free-cus", type=int, default=-1,
+                    help="c3: CUs the cross-covariance stream leaves free (-1: library default)")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
     ap.add_argument("--c4-path", choices=("fit_predict", "predict"), default="predict",
                     help="c4: gram -> potrf -> gp_predict (default), or one gp_fit_predict per "
@@ -196,7 +200,8 @@ def main():
     bd = torch.as_tensor(beta, device=dev).reshape(1, d)
     sd = torch.tensor([s], dtype=torch.float64, device=dev)
     dd = torch.tensor([delta], dtype=torch.float64, device=dev)
-    fctx = None if args.serial else kernels.FitPredictContext(dev)
+    fctx = None if args.serial else kernels.FitPredictContext(dev, args.cross_start,
+                                                              args.aux_free_cus)
     ws = kernels.PredictWorkspace()
     out = torch.empty((2, ml), dtype=torch.float64, device=dev)   # rows: mean, var
 

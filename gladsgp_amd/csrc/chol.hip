@@ -1435,9 +1435,14 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
 // The early tasks are what the chain waits on (its partials and the near-diagonal tiles the
 // partials wait on): they are dequeued kPPLead = W chain steps ahead of their topological
 // position, early enough to catch up on their K steps that are already available.  Only
-// early tasks can wait on tasks not yet dequeued, and at most ~W (2 + kPPBand) of them wait at
-// a time, far fewer than the workers, so the order stays deadlock-free.
+// early tasks can wait on tasks not yet dequeued: per problem, those dequeued in the last 4W
+// keys (W DP, W SP, 2W band LT).  With W = 0 the list is topological: every worker task waits
+// only on earlier tasks and on chain steps whose own inputs are earlier still, so any grid with
+// more workgroups than problems drains.  pp_lead() takes W = kPPLead only while every problem's
+// blocked early tasks plus its chain fit in the grid with a worker to spare (batch 32 at
+// n = 1024 on 256 workgroups deadlocked with W = 6 for every problem: 32 x 24 > 224).
 constexpr int kPPLead = 6;
+constexpr int kPPLeadBlocked = 4 * kPPLead + 2;   // per-problem bound on blocked early tasks
 constexpr int kPPBand = 3;
 
 // LT tiles (s - j, j) on anti-diagonal s with band (i - j <= kPPBand) or not: j range.
@@ -1452,7 +1457,7 @@ GP_DEV void pp_lt_range(int s, int N, bool band, int& jmin, int& jmax) {
   if (s < 2) jmax = -1;
 }
 
-__device__ int pp_key_count(int t, int N, bool inv) {
+__device__ int pp_key_count(int t, int N, bool inv, int lead) {
   int c = 0, jmin, jmax;
   if (t % 4 == 2 && (t + 2) / 4 >= 2 && (t + 2) / 4 <= N - 1) ++c;            // DP
   if (t % 4 == 1 && (t - 1) / 4 >= 1 && (t - 1) / 4 <= N - 2) ++c;            // SP
@@ -1460,7 +1465,7 @@ __device__ int pp_key_count(int t, int N, bool inv) {
     pp_lt_range(t / 2, N, true, jmin, jmax);
     c += max(0, jmax - jmin + 1);
   }
-  const int K = t - 4 * kPPLead;
+  const int K = t - 4 * lead;
   if (K < 0) return c;
   if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) c += (K - 2) / 4;  // XT
   if (K % 2 == 0) {                                                            // other LT
@@ -1471,11 +1476,11 @@ __device__ int pp_key_count(int t, int N, bool inv) {
 }
 
 __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, int batch,
-                                                           int inv) {
+                                                           int inv, int lead) {
   __shared__ int cnt[2][1024];
   const int T = threadIdx.x;
-  const int nk = 4 * N - 1 + 4 * kPPLead;
-  const int own = T < nk ? pp_key_count(T, N, inv != 0) : 0;
+  const int nk = 4 * N - 1 + 4 * lead;
+  const int own = T < nk ? pp_key_count(T, N, inv != 0, lead) : 0;
   cnt[0][T] = own;
   __syncthreads();
   int src = 0;
@@ -1498,7 +1503,7 @@ __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, i
     pp_lt_range(T / 2, N, true, jmin, jmax);
     for (int j = jmax; j >= jmin; --j) emit(kTL, T / 2 - j, j);
   }
-  const int K = T - 4 * kPPLead;
+  const int K = T - 4 * lead;
   if (K < 0) return;
   if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) {
     const int i = (K - 2) / 4;
@@ -1582,6 +1587,12 @@ static int num_cus() {
   return ncu;
 }
 
+// Dequeue lead (see pp_schedule_kernel): W = kPPLead while every problem's chain and blocked
+// early tasks leave a worker free, else the topological order (W = 0).
+static int pp_lead(int batch, int grid) {
+  return (long long)batch * (kPPLeadBlocked + 1) < grid ? kPPLead : 0;
+}
+
 // The persistent dataflow factorisation (pp_kernel) on `stream`: stream-ordered scratch for the
 // task list, the dequeue head and the per-tile flags (hipMallocAsync / hipFreeAsync), one
 // schedule launch, one persistent launch with one workgroup per CU.  X is L^-1 (inv, zeroed by
@@ -1599,8 +1610,10 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   int2* tasks = reinterpret_cast<int2*>(scr);
   int* head = reinterpret_cast<int*>(scr + task_bytes);
   int* flags = reinterpret_cast<int*>(scr + task_bytes + 256);
+  const int grid = (int)(ntasks < num_cus() ? ntasks : num_cus());
+  const int lead = pp_lead(batch, grid);
   hipLaunchKernelGGL(pp_schedule_kernel, dim3(1), dim3(1024), 0, stream, tasks, N, batch,
-                     inv ? 1 : 0);
+                     inv ? 1 : 0, lead);
   GP_CK(hipGetLastError());
   PPArgs P;
   P.A = A; P.sA = sA; P.lda = lda;
@@ -1613,7 +1626,6 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   P.dbg = dbg ? reinterpret_cast<int*>(std::strtoull(dbg, nullptr, 0)) : nullptr;
   const char* trc = std::getenv("GPFIT_PP_TRACE_PTR");   // debug only: device int64 buffer
   P.trace = trc ? reinterpret_cast<long long*>(std::strtoull(trc, nullptr, 0)) : nullptr;
-  const int grid = (int)(ntasks < num_cus() ? ntasks : num_cus());
   hipLaunchKernelGGL(pp_kernel, dim3(grid), dim3(256), 0, stream, P);
   GP_CK(hipGetLastError());
   GP_CK(hipFreeAsync(scr, stream));
@@ -1622,8 +1634,9 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
 
 static bool pp_eligible(int n, int batch) {
   const int N = gp_ceil_div(n, NB);
+  // the chains hold `batch` workgroups for the whole launch: at least as many workers again
   return N <= kPPMaxN && pp_task_count(N, true) * (long long)batch < (1ll << 30) &&
-         std::getenv("GPFIT_POTRF_SWEEP") == nullptr;
+         2 * batch <= num_cus() && std::getenv("GPFIT_POTRF_SWEEP") == nullptr;
 }
 
 // Zero L^-1 (upper triangle + padding): one memset for a packed batch, else one 2-D memset per
@@ -1667,8 +1680,13 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
   gpfit_prof_begin(GP_PROF_POTRF, stream);
   int rc;
   if (pp_eligible(n, batch)) {
+    // one launch, no block steps: an event asked for at a step inside the factorisation is
+    // recorded before the launch (whatever waits on it runs beside the whole factorisation),
+    // one asked for at k_ev >= N after it
+    const int N = gp_ceil_div(n, NB);
+    if (ev && k_ev >= 0 && k_ev < N) GP_CK(hipEventRecord(ev, stream));
     rc = pp_factor(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet, true, stream);
-    if (rc == 0 && ev) GP_CK(hipEventRecord(ev, stream));
+    if (rc == 0 && ev && !(k_ev >= 0 && k_ev < N)) GP_CK(hipEventRecord(ev, stream));
   } else {
     rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,
                                 stream, k_ev, ev);

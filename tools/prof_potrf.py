@@ -1,17 +1,33 @@
-"""Profile target: gram + potrf_inv at n (default 4096) a few times."""
-import sys, time
+"""Profile target: gram + potrf_inv at n (default 4096), `batch` problems, a few times.
+
+    python tools/prof_potrf.py [n] [reps] [batch]
+"""
+import os
+import sys
+import time
+
 import numpy as np
 import torch
-import os; sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from gladsgp_amd import kernels
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gladsgp_amd import kernels  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+batch = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 dev = torch.device("cuda:0")
 X = torch.as_tensor(np.random.default_rng(0).random((n, 8)), device=dev)
-beta = torch.as_tensor(np.random.default_rng(3).uniform(0.5, 5, 8), device=dev)
+beta = torch.as_tensor(np.stack([np.random.default_rng(10 + j).uniform(0.5, 5, 8)
+                                 for j in range(batch)]), device=dev)
+ones = torch.ones(batch, dtype=torch.float64, device=dev)
+ts = []
 for r in range(reps):
-    torch.cuda.synchronize(); t0 = time.perf_counter()
-    ch = kernels.cholesky_inverse(kernels.gram(X, beta, 1.0, 1e-6))
-    torch.cuda.synchronize(); print(f"rep {r}: {1e3*(time.perf_counter()-t0):.3f} ms", flush=True)
+    G = kernels.gram(X, beta, ones, 1e-6 * ones, batch=batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ch = kernels.cholesky_inverse(G)
+    torch.cuda.synchronize()
+    ts.append(1e3 * (time.perf_counter() - t0))
+    print(f"rep {r}: potrf_inv {ts[-1]:.3f} ms", flush=True)
 ch.check()
+print(f"n={n} batch={batch} min {min(ts):.3f} ms median {sorted(ts)[len(ts) // 2]:.3f} ms")
