@@ -42,8 +42,15 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
         return LIB_PATH
     os.makedirs(OBJ_DIR, exist_ok=True)
 
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(PKG_DIR, "..", "include", "gpfit.h"))
+    t_hdr = max(os.path.getmtime(h) for h in headers if os.path.exists(h))
+
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJ_DIR, src.replace(".hip", ".o"))
+        if (not force and os.path.exists(obj) and
+                os.path.getmtime(obj) > max(t_hdr, os.path.getmtime(os.path.join(CSRC, src)))):
+            return obj                  # up to date: sources and headers older than the object
         cmd = [HIPCC] + FLAGS + EXTRA.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

@@ -2,15 +2,22 @@
 //
 // One kernel serves both (reference: examples/01...ipynb:135-141, SEPIA compute_cov_mat):
 //   out[i + j*ldo] = s * exp(-sum_k beta_k (XA[i,k] - XB[j,k])^2) + delta*(i==j && diag)
-// A block of 4 waves owns a 64 x 64 output tile; lane = row, so each wave stores 64
-// consecutive doubles (512 B) per column: fully coalesced column-major writes.  The row design
-// vector lives in registers; each wave walks its 16 columns, whose design vectors are
-// wave-uniform scalar loads.  A square Gram can be built lower-triangle only (the grid then
-// enumerates the tiles on and below the diagonal), which is all the factorisation reads.
+// Work unit = one output column segment of a 64-row tile: 64 rows (lane = row, so a wave
+// stores 512 contiguous bytes per unit) x 1 column.  The units of the whole job (every problem
+// of the batch; the tiles on and below the diagonal only for a lower-triangle Gram) are cut into
+// one contiguous range per wave of a grid sized to the chip's residency, so every wave runs the
+// same number of units (+-1) in ONE residency round (the 64 x 64-tile grid it replaces put 2080
+// blocks on 1792 block slots at n = 4096: a second round for 288 blocks doubled the kernel).
+// Per range, a wave stages the design vectors of its next 64 / (D/8) columns through LDS (one
+// lane-linear load, then wave-uniform broadcast reads: the "d-tile"), keeps its row's design
+// vector and beta in registers, and walks its units in order, reloading them only when the
+// (problem, row tile) changes.
 //
-// Roofline: 8 B written per output element + 8 d B read per row/col vector (amortised);
-// one f64 exp (~1.3 T exp/s chip-wide, probe_f64) per element — the store stream (≈6 TB/s =
-// 0.75 T elements/s) is the bound.
+// Roofline: 8 B written per output element + 8 d B read per row/column vector (amortised),
+// and per element ~45 fp64 VALU ops (3 d for the weighted distance, 18 for exp_neg, the
+// store address).  At n = 4096 (lower triangle, 133k column units of 64 elements) the stores
+// alone take 12.3 us (5.5 TB/s) and the arithmetic alone 17 us in tools/dbg/gram_micro.hip:
+// the kernel is bound by the fp64 VALU pipe, not by HBM (profiles/r02/gram_micro.txt).
 #include "gpfit_common.h"
 #include "gpfit_profile.h"
 #include "gpfit_internal.h"
@@ -18,10 +25,66 @@
 
 namespace {
 
-constexpr int kTile = 64;    // output tile kTile x kTile per block of 4 waves
-constexpr int kWCols = 16;   // columns per wave (lane = row)
+constexpr int kTile = 64;        // rows per unit (lane = row) and columns per tile
+constexpr int kWaves = 4;        // waves per block
 
-// Block (ti, tj) of the output; with `lower`, blockIdx.x enumerates the tiles tj <= ti only.
+
+struct GramShape {
+  int TR, TC;                    // tiles down / across
+  int tiles;                     // tiles per problem (lower: TR (TR + 1) / 2)
+  int units;                     // tiles * 64 per problem
+  bool lower;
+};
+
+// Tile t of a problem -> (ti, tj); lower: t enumerates tj <= ti row by row.
+GP_DEV void tile_of(const GramShape& g, int t, int& ti, int& tj) {
+  if (g.lower) {
+    int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while (r * (r + 1) / 2 > t) --r;
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    ti = r;
+    tj = t - r * (r + 1) / 2;
+  } else {
+    ti = t / g.TC;
+    tj = t - ti * g.TC;
+  }
+}
+
+// exp(-a) for a >= 0 (a weighted squared distance), ~19 VALU ops: Cody-Waite reduction by ln 2,
+// a degree-11 minimax polynomial for e^r (|r| <= ln2/2; the coefficients ocml's exp uses), and
+// ldexp.  Every polynomial step is fma(p, r, c) with c a wave-uniform constant (an SGPR or
+// literal operand), so no constant has to be re-materialised in a VGPR per call (ocml's fmac
+// form overwrites its constant registers: 22 extra v_mov per exp inside a loop).  a is clamped
+// to 1100 first: e^-1100 underflows to +0 through the ldexp, the only range check a
+// non-negative argument needs.  Accuracy: within 1 ulp of exp (the same reduction and
+// polynomial as ocml).
+// fma(p, r, c) with c wave-uniform, pinned to VOP3 v_fma_f64 with c in an SGPR pair (the
+// compiler otherwise keeps c in a VGPR and copies it before every v_fmac_f64).
+GP_DEV double fma_sc(double p, double r, double c) {
+  double o;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(p), "v"(r), "s"(c));
+  return o;
+}
+
+GP_DEV double exp_neg(double a) {
+  const double x = -fmin(a, 1100.0);
+  const double k = __builtin_rint(x * 0x1.71547652b82fep+0);              // x log2(e)
+  double r = fma(k, -0x1.62e42fefa39efp-1, x);                             // - k ln2 (hi)
+  r = fma(k, -0x1.abc9e3b39803fp-56, r);                                   // - k ln2 (lo)
+  double p = fma_sc(r, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+  p = fma_sc(p, r, 0x1.71dee623fde64p-19);
+  p = fma_sc(p, r, 0x1.a01997c89e6b0p-16);
+  p = fma_sc(p, r, 0x1.a01a014761f6ep-13);
+  p = fma_sc(p, r, 0x1.6c16c1852b7b0p-10);
+  p = fma_sc(p, r, 0x1.1111111122322p-7);
+  p = fma_sc(p, r, 0x1.55555555502a1p-5);
+  p = fma_sc(p, r, 0x1.5555555555511p-3);
+  p = fma_sc(p, r, 0x1.000000000000bp-1);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return __builtin_ldexp(p, (int)k);
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void ardse_kernel(
     const double* __restrict__ XA, int na, int ldxa,      // row points (output rows)
@@ -29,54 +92,110 @@ __global__ __launch_bounds__(256) void ardse_kernel(
     int d, const double* __restrict__ beta, int ldbeta,
     const double* __restrict__ s, const double* __restrict__ delta,
     double* __restrict__ out, int ldo, long long stride_o,
-    int rows_out, int cols_out, bool lower) {
-  const int b = blockIdx.z;
-  int ti, tj;
-  if (lower) {
-    const int t = blockIdx.x;
-    ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while (ti * (ti + 1) / 2 > t) --ti;
-    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-    tj = t - ti * (ti + 1) / 2;
-  } else {
-    ti = blockIdx.x;
-    tj = blockIdx.y;
-  }
+    int rows_out, int cols_out, GramShape g, int total) {
+  __shared__ __attribute__((aligned(16))) double xs_all[kWaves][kTile * D];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i = ti * kTile + lane;
-  const int jw = tj * kTile + w * kWCols;          // this wave's first column (uniform)
-  const double* bb = beta + (long long)b * ldbeta;
-  double bet[D], xa[D];
-  const int ic = i < na ? i : na - 1;
+  double* xs = xs_all[w];
+  const long long nw = (long long)gridDim.x * kWaves;
+  const long long gw = (long long)blockIdx.x * kWaves + w;
+  int u = (int)(total * gw / nw);
+  const int u1 = (int)(total * (gw + 1) / nw);
+  int cur_b = -1, cur_ti = -1;
+  double xa[D], sb = 0.0, db = 0.0;
+  const double* bb = beta;
+  while (u < u1) {
+    // one segment: units u .. u + len - 1 share the problem b and the tile (ti, tj)
+    const int b = u / g.units;
+    const int rem = u - b * g.units;
+    const int t = rem / kTile, c0 = rem - t * kTile;
+    const int len = min(kTile - c0, u1 - u);
+    int ti, tj;
+    tile_of(g, t, ti, tj);
+    if (b != cur_b || ti != cur_ti) {                    // this lane's row vector, beta, s, delta
+      bb = beta + (long long)b * ldbeta;
+      const int ic = min(ti * kTile + lane, na - 1);
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    bet[k] = k < d ? bb[k] : 0.0;
-    xa[k] = k < d ? XA[(long long)ic * ldxa + k] : 0.0;
-  }
-  const double sb = s[b];
-  const double db = delta ? delta[b] : 0.0;
-  double* o = out + (long long)b * stride_o + i;
-  const bool row_st = i < rows_out;
-  const bool row_ok = i < na;
-#pragma unroll 4
-  for (int c = 0; c < kWCols; ++c) {
-    const int j = jw + c;                          // uniform
-    if (j >= cols_out) break;
-    double v = 0.0;
-    if (j < nb) {
-      const double* xb = XB + (long long)j * ldxb;  // uniform: scalar loads
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        const double t = xa[k] - (k < d ? xb[k] : 0.0);
-        acc = fma(bet[k] * t, t, acc);
-      }
-      v = fma(sb, exp(-acc), (i == j) ? db : 0.0);
-      v = row_ok ? v : 0.0;
+      for (int k = 0; k < D; ++k) xa[k] = k < d ? XA[(long long)ic * ldxa + k] : 0.0;
+      sb = s[b];
+      db = delta ? delta[b] : 0.0;
+      cur_b = b;
+      cur_ti = ti;
     }
-    if (row_st && (!lower || j <= i)) o[(long long)j * ldo] = v;
+    double bet[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) bet[k] = k < d ? bb[k] : 0.0;
+    // the d-tile: lane l stages column tj*64 + l's design vector, read back as broadcasts
+    const int j0 = tj * kTile;
+    __builtin_amdgcn_wave_barrier();
+    {
+      const int j = j0 + lane;
+      const bool ok = lane >= c0 && lane < c0 + len && j < nb;
+      const double* src = XB + (long long)(ok ? j : 0) * ldxb;
+#pragma unroll
+      for (int k = 0; k < D; ++k) xs[lane * D + k] = (ok && k < d) ? src[k] : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int i = ti * kTile + lane;
+    const int cend = min(c0 + len, cols_out - j0);      // columns this segment stores
+    double* o = out + (long long)b * stride_o + i;
+    // interior segment (every row and column valid, strictly below the diagonal of a lower
+    // Gram or off the diagonal tile, no jitter term): no per-element selects or store masks
+    const bool interior = ti * kTile + kTile <= min(na, rows_out) && j0 + cend <= nb &&
+                          (g.lower ? tj < ti : (ti != tj || !delta));
+    if (interior) {
+      for (int c = c0; c < cend; ++c) {
+        const double* xb = xs + c * D;                   // wave-uniform: broadcast reads
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const double dt = xa[k] - xb[k];
+          acc = fma(bet[k] * dt, dt, acc);
+        }
+        o[(long long)(j0 + c) * ldo] = sb * exp_neg(acc);
+      }
+    } else {
+      const bool row_ok = i < na, row_st = i < rows_out;
+      for (int c = c0; c < cend; ++c) {
+        const int j = j0 + c;
+        const double* xb = xs + c * D;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const double dt = xa[k] - xb[k];
+          acc = fma(bet[k] * dt, dt, acc);
+        }
+        double v = fma(sb, exp_neg(acc), (i == j) ? db : 0.0);
+        v = (row_ok && j < nb) ? v : 0.0;
+        if (row_st && (!g.lower || j <= i)) o[(long long)j * ldo] = v;
+      }
+    }
+    u += len;
   }
+}
+
+template <int D>
+int ardse_blocks_per_cu() {
+  static const int occ = [] {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ardse_kernel<D>, 256, 0) !=
+            hipSuccess || nb <= 0)
+      nb = 4;
+    return nb;
+  }();
+  return occ;
+}
+
+int gram_num_cus() {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    return n;
+  }();
+  return ncu;
 }
 
 template <int D>
@@ -84,11 +203,23 @@ hipError_t launch_ardse(const double* XA, int na, int ldxa, const double* XB, in
                         int d, const double* beta, int ldbeta, const double* s,
                         const double* delta, double* out, int ldo, long long stride_o,
                         int rows_out, int cols_out, int batch, bool lower, hipStream_t st) {
-  const int TR = gp_ceil_div(rows_out, kTile), TC = gp_ceil_div(cols_out, kTile);
-  dim3 grid = lower ? dim3(TR * (TR + 1) / 2, 1, batch) : dim3(TR, TC, batch);
-  hipLaunchKernelGGL((ardse_kernel<D>), grid, dim3(256), 0, st, XA, na, ldxa, XB, nb, ldxb,
-                     d, beta, ldbeta, s, delta, out, ldo, stride_o, rows_out, cols_out,
-                     lower);
+  GramShape g;
+  g.TR = gp_ceil_div(rows_out, kTile);
+  g.TC = gp_ceil_div(cols_out, kTile);
+  g.lower = lower;
+  const long long tiles = lower ? (long long)g.TR * (g.TR + 1) / 2 : (long long)g.TR * g.TC;
+  const long long total = tiles * kTile * batch;
+  if (total >= (1LL << 31)) return hipErrorInvalidValue;   // > 16 G output elements
+  g.tiles = (int)tiles;
+  g.units = (int)(tiles * kTile);
+  // one residency round: every wave of the grid is resident at once (or the grid is smaller
+  // than that, when there are fewer than ~8 units per wave)
+  const long long cap = (long long)gram_num_cus() * ardse_blocks_per_cu<D>();
+  const long long want = gp_ceil_div(total, 8LL * kWaves);
+  const int grid = (int)(want < cap ? want : cap);
+  hipLaunchKernelGGL((ardse_kernel<D>), dim3(grid), dim3(256), 0, st, XA, na, ldxa, XB, nb, ldxb,
+                     d, beta, ldbeta, s, delta, out, ldo, stride_o, rows_out, cols_out, g,
+                     (int)total);
   return hipGetLastError();
 }
 
