@@ -31,6 +31,7 @@
 #include "gpfit_internal.h"
 #include "../../include/gpfit.h"
 
+#define GP_HD __host__ __device__
 
 namespace {
 
@@ -136,6 +137,29 @@ GP_DEV void mma64(const double* As, const double* Bs, f64x4 (&acc)[2][2]) {
     const int k = k4 + (NB / 4) * lk;
     const double a0 = As[k * LP + wr * 32 + li], a1 = As[k * LP + wr * 32 + 16 + li];
     const double b0 = Bs[k * LP + wc * 32 + li], b1 = Bs[k * LP + wc * 32 + 16 + li];
+    acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
+    acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
+    acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
+    acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+  }
+}
+
+// mma64 with the B operand read transposed: acc = sum_k As[k][rows] * Bt[cols][k] (Bt held
+// [row][col], e.g. a factor tile as diag_factor_blk leaves it).  Lanes li of a fragment read
+// sit LP = 65 doubles apart: 16 distinct bank pairs, and the k slots 16 apart put the other
+// lane groups on the other 32 banks (conflict-free).
+GP_DEV void mma64_bt(const double* As, const double* Bt, f64x4 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = zero4();
+#pragma unroll 4
+  for (int k4 = 0; k4 < NB / 4; ++k4) {
+    const int k = k4 + (NB / 4) * lk;
+    const double a0 = As[k * LP + wr * 32 + li], a1 = As[k * LP + wr * 32 + 16 + li];
+    const double b0 = Bt[(wc * 32 + li) * LP + k], b1 = Bt[(wc * 32 + 16 + li) * LP + k];
     acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
     acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
     acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
@@ -1075,6 +1099,15 @@ GP_DEV bool pp_wait1(const int* f, int* abort) {
   return ok != 0;
 }
 
+// Whether the flag *f is set now (no waiting); one lane reads, the workgroup gets the answer.
+GP_DEV bool pp_test1(const int* f) {
+  if (threadIdx.x == 0) g_msg[3] = pp_ldflag(f) != 0;
+  __syncthreads();
+  const int ok = g_msg[3];
+  __syncthreads();
+  return ok != 0;
+}
+
 // One K step of a worker task: opA tile (NAT), opB tile (NAT or TRN), the two producer flags.
 struct PPTerm {
   const double *a, *b;
@@ -1299,6 +1332,8 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
   double* Ab = P.A + b * P.sA;
   auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
   double ld_sum = 0.0;
+  OpTile tpj;                // P_jj, loaded by the previous step when its partials were ready
+  bool pref = false;
   for (int j = 0; j < N; ++j) {
     const int nb = min(NB, P.n - j * NB);
     PP_MARK(P, 10, j);
@@ -1307,10 +1342,11 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
     // (a) C_jj = P_jj - L_j,j-1 L_j,j-1^T into As as a full symmetric [row][col] tile.  The
     // P_jj loads (16-B sc1, the whole tile; only its lower triangle is used) are in flight
     // during the SYRK.
-    if (j >= 2 && !pp_wait1(F + 2 * N * N + j, abort)) return;
+    if (!pref) {
+      if (j >= 2 && !pp_wait1(F + 2 * N * N + j, abort)) return;
+      pp_load(tpj, atile(j, j), P.lda, nb, nb);
+    }
     PP_TRACE(P, tb0 + 1, pp_now());
-    OpTile tpj;
-    pp_load(tpj, atile(j, j), P.lda, nb, nb);
     f64x4 acc[2][2];
     if (j >= 1) mma64(g_keep, g_keep, acc);
     else {
@@ -1366,21 +1402,19 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
     PP_TRACE(P, tb0 + 5, pp_now());
     OpTile tp;
     pp_load(tp, atile(j + 1, j), P.lda, nb1, NB);      // As[p][r] = P[r][p]
-    // D_j^T: Bs[p][c] = D[c][p] from Bs[row][col] = D[row][col] (in-place transpose)
-    for (int g = threadIdx.x; g < NB * NB; g += 256) {
-      const int r = g & (NB - 1), c = g >> 6;
-      if (r > c) {
-        const double x = sm.Bs[r * LP + c], y = sm.Bs[c * LP + r];
-        sm.Bs[r * LP + c] = y;
-        sm.Bs[c * LP + r] = x;
-      }
+    // the next step's P_j+1,j+1, in flight under this step's GEMM and stores when its partial
+    // sums are already published
+    pref = j + 1 < 2 || pp_test1(F + 2 * N * N + j + 1);
+    if (pref) {
+      const int nbn = min(NB, P.n - (j + 1) * NB);
+      pp_load(tpj, atile(j + 1, j + 1), P.lda, nbn, nbn);
     }
     __syncthreads();
     store_op<false>(sm.As, tp);
     __syncthreads();
     PP_MARK(P, 14, j);
     PP_TRACE(P, tb0 + 6, pp_now());
-    mma64(sm.As, sm.Bs, acc);
+    mma64_bt(sm.As, sm.Bs, acc);                       // P D^T, D held [row][col] in Bs
     __syncthreads();
     acc_to_lds(g_keep, acc);                           // keep[c][r] = L_j+1,j(r, c)
     __syncthreads();
@@ -1445,42 +1479,42 @@ constexpr int kPPLead = 6;
 constexpr int kPPLeadBlocked = 4 * kPPLead + 2;   // per-problem bound on blocked early tasks
 constexpr int kPPBand = 3;
 
-// LT tiles (s - j, j) on anti-diagonal s with band (i - j <= kPPBand) or not: j range.
-GP_DEV void pp_lt_range(int s, int N, bool band, int& jmin, int& jmax) {
-  jmin = max(0, s - (N - 1));
-  if (band) {
-    jmin = max(jmin, (s - kPPBand + 1) / 2);   // s - 2j <= kPPBand
-    jmax = (s - 2) / 2;                         // s - 2j >= 2
-  } else {
-    jmax = s >= kPPBand + 1 ? (s - kPPBand - 1) / 2 : -1;   // s - 2j >= kPPBand + 1
-  }
-  if (s < 2) jmax = -1;
-}
-
-__device__ int pp_key_count(int t, int N, bool inv, int lead) {
-  int c = 0, jmin, jmax;
-  if (t % 4 == 2 && (t + 2) / 4 >= 2 && (t + 2) / 4 <= N - 1) ++c;            // DP
-  if (t % 4 == 1 && (t - 1) / 4 >= 1 && (t - 1) / 4 <= N - 2) ++c;            // SP
-  if (t % 2 == 0) {                                                            // band LT
-    pp_lt_range(t / 2, N, true, jmin, jmax);
-    c += max(0, jmax - jmin + 1);
+// The tasks of key t in emission order (f(kind, i, j) per task; see pp_schedule_kernel):
+//   early  DP(j): t = 4j-2;  SP(j): t = 4j+1;  band LT(i,j), 2 <= i-j <= kPPBand: t = 2(i+j)
+//   late   (K = t - 4W)  XT(i,c): K = 4i+2;  LT(i,j), i-j > kPPBand: K = 2(i+j)
+// Every input of a late task has a smaller key or is a chain step whose own inputs do (see the
+// section comment).  Shared by the schedule kernel (count + emit) and the host's task count.
+template <typename F>
+GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, F&& f) {
+  if (t % 4 == 2 && (t + 2) / 4 >= 2 && (t + 2) / 4 <= N - 1) f(kTDP, 0, (t + 2) / 4);
+  if (t % 4 == 1 && (t - 1) / 4 >= 1 && (t - 1) / 4 <= N - 2) f(kTSP, (t - 1) / 4 + 1, (t - 1) / 4);
+  if (t % 2 == 0 && t >= 4) {                                  // band LT on anti-diagonal s
+    const int s = t / 2;
+    const int jmin = (s - kPPBand + 1) / 2 > s - (N - 1) ? (s - kPPBand + 1) / 2 : s - (N - 1);
+    for (int j = (s - 2) / 2; j >= jmin && j >= 0; --j) f(kTL, s - j, j);
   }
   const int K = t - 4 * lead;
-  if (K < 0) return c;
-  if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) c += (K - 2) / 4;  // XT
-  if (K % 2 == 0) {                                                            // other LT
-    pp_lt_range(K / 2, N, false, jmin, jmax);
-    c += max(0, jmax - jmin + 1);
+  if (K < 0) return;
+  if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) {
+    const int i = (K - 2) / 4;
+    for (int c = i - 1; c >= 0; --c) f(kTX, i, c);             // nearest the diagonal first
   }
-  return c;
+  if (K % 2 == 0) {                                            // late LT singles
+    const int s = K / 2;
+    const int jmin = s - (N - 1) > 0 ? s - (N - 1) : 0;
+    for (int j = (s - kPPBand - 1) / 2; j >= jmin && s >= kPPBand + 1; --j) f(kTL, s - j, j);
+  }
 }
+
+GP_HD inline int pp_nkeys(int N, int lead) { return 4 * N - 1 + 4 * lead; }
 
 __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, int batch,
                                                            int inv, int lead) {
   __shared__ int cnt[2][1024];
   const int T = threadIdx.x;
-  const int nk = 4 * N - 1 + 4 * lead;
-  const int own = T < nk ? pp_key_count(T, N, inv != 0, lead) : 0;
+  const int nk = pp_nkeys(N, lead);
+  int own = 0;
+  if (T < nk) pp_for_key(T, N, inv != 0, lead, [&](int, int, int) { ++own; });
   cnt[0][T] = own;
   __syncthreads();
   int src = 0;
@@ -1493,33 +1527,17 @@ __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, i
   if (T >= nk) return;
   const int excl = cnt[src][T] - own;
   long long pos = batch + (long long)excl * batch;
-  auto emit = [&](int kind, int i, int j) {
+  pp_for_key(T, N, inv != 0, lead, [&](int kind, int i, int j) {
     for (int b = 0; b < batch; ++b) tasks[pos++] = make_int2(kind | (b << 4), i | (j << 16));
-  };
-  int jmin, jmax;
-  if (T % 4 == 2 && (T + 2) / 4 >= 2 && (T + 2) / 4 <= N - 1) emit(kTDP, 0, (T + 2) / 4);
-  if (T % 4 == 1 && (T - 1) / 4 >= 1 && (T - 1) / 4 <= N - 2) emit(kTSP, (T - 1) / 4 + 1, (T - 1) / 4);
-  if (T % 2 == 0) {
-    pp_lt_range(T / 2, N, true, jmin, jmax);
-    for (int j = jmax; j >= jmin; --j) emit(kTL, T / 2 - j, j);
-  }
-  const int K = T - 4 * lead;
-  if (K < 0) return;
-  if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) {
-    const int i = (K - 2) / 4;
-    for (int c = i - 1; c >= 0; --c) emit(kTX, i, c);   // nearest the diagonal first
-  }
-  if (K % 2 == 0) {
-    pp_lt_range(K / 2, N, false, jmin, jmax);
-    for (int j = jmax; j >= jmin; --j) emit(kTL, K / 2 - j, j);
-  }
+  });
 }
 
+// Tasks per problem, chain included (host side of the same enumeration; any lead gives the
+// same total).
 long long pp_task_count(int N, bool inv) {
-  const long long lt = (long long)(N - 1) * (N - 2) / 2;
-  const long long dp = N >= 3 ? N - 2 : 0, sp = N >= 3 ? N - 2 : 0;
-  const long long xt = inv ? (long long)N * (N - 1) / 2 : 0;
-  return 1 + lt + dp + sp + xt;
+  long long c = 1;
+  for (int t = 0; t < pp_nkeys(N, 0); ++t) pp_for_key(t, N, inv, 0, [&](int, int, int) { ++c; });
+  return c;
 }
 
 }  // namespace
@@ -1604,13 +1622,13 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   const int fstride = ((2 * N * N + 2 * N + 1 + 31) / 32) * 32;
   const size_t task_bytes = ((size_t)ntasks * sizeof(int2) + 255) / 256 * 256;
   const size_t flag_bytes = 256 + (size_t)batch * fstride * sizeof(int);
+  const int grid = (int)(ntasks < num_cus() ? ntasks : num_cus());
   char* scr = nullptr;
   GP_CK(hipMallocAsync(reinterpret_cast<void**>(&scr), task_bytes + flag_bytes, stream));
   GP_CK(hipMemsetAsync(scr + task_bytes, 0, flag_bytes, stream));
   int2* tasks = reinterpret_cast<int2*>(scr);
   int* head = reinterpret_cast<int*>(scr + task_bytes);
   int* flags = reinterpret_cast<int*>(scr + task_bytes + 256);
-  const int grid = (int)(ntasks < num_cus() ? ntasks : num_cus());
   const int lead = pp_lead(batch, grid);
   hipLaunchKernelGGL(pp_schedule_kernel, dim3(1), dim3(1024), 0, stream, tasks, N, batch,
                      inv ? 1 : 0, lead);

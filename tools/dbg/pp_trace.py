@@ -8,31 +8,39 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N = (n + 63) // 64
 W, B = 6, 3  # chol.hip kPPLead, kPPBand
-def lt_range(s, band):
-    jmin = max(0, s - (N - 1))
-    if band:
-        jmin = max(jmin, (s - B + 1) // 2); jmax = (s - 2) // 2
-    else:
-        jmax = (s - B - 1) // 2
-    return (jmin, jmax) if s >= 2 else (0, -1)
+NBf = 0   # no block tasks
+in_ltb = lambda i, j: (i >> 1) < NBf and (i >> 1) - (j >> 1) >= 3
+in_xtb = lambda i, c: (i >> 1) < NBf and (i >> 1) > (c >> 1)
 tasks = [("C", 0, 0)]
-for T in range(4 * N - 1 + 4 * W):
-    if T % 4 == 2 and 2 <= (T + 2) // 4 <= N - 1: tasks.append(("DP", 0, (T + 2) // 4))
-    if T % 4 == 1 and 1 <= (T - 1) // 4 <= N - 2: tasks.append(("SP", (T - 1) // 4 + 1, (T - 1) // 4))
-    if T % 2 == 0:
-        a, b = lt_range(T // 2, True)
-        tasks += [("L", T // 2 - j, j) for j in range(b, a - 1, -1)]
-    K = T - 4 * W
+for t in range(4 * N - 1 + 4 * W):          # chol.hip pp_for_key
+    if t % 4 == 2 and 2 <= (t + 2) // 4 <= N - 1: tasks.append(("DP", 0, (t + 2) // 4))
+    if t % 4 == 1 and 1 <= (t - 1) // 4 <= N - 2: tasks.append(("SP", (t - 1) // 4 + 1, (t - 1) // 4))
+    if t % 2 == 0 and t >= 4:
+        s_ = t // 2
+        jmin = max((s_ - B + 1) // 2, s_ - (N - 1))
+        tasks += [("L", s_ - j, j) for j in range((s_ - 2) // 2, max(jmin, 0) - 1, -1)]
+    K = t - 4 * W
     if K < 0: continue
     if K % 4 == 2 and 1 <= (K - 2) // 4 <= N - 1:
         i = (K - 2) // 4
-        tasks += [("X", i, c) for c in range(i - 1, -1, -1)]
+        tasks += [("X", i, c) for c in range(i - 1, -1, -1) if not in_xtb(i, c)]
+    if K % 8 == 2 and 1 <= (K - 2) // 8 < NBf:
+        I = (K - 2) // 8
+        tasks += [("XB", I, C) for C in range(I - 1, -1, -1)]
     if K % 2 == 0:
-        a, b = lt_range(K // 2, False)
-        tasks += [("L", K // 2 - j, j) for j in range(b, a - 1, -1)]
+        s_ = K // 2
+        jmin = max(s_ - (N - 1), 0)
+        if s_ >= B + 1:
+            tasks += [("L", s_ - j, j) for j in range((s_ - B - 1) // 2, jmin - 1, -1)
+                      if not in_ltb(s_ - j, j)]
+    if K % 4 == 0:
+        S = K // 4
+        jlo = max(S - NBf + 1, 0)
+        if S >= 3:
+            tasks += [("LB", S - J, J) for J in range((S - 3) // 2, jlo - 1, -1)]
 nt = len(tasks)
 dev = torch.device("cuda:0")
-trace = torch.zeros(nt * 4 + N * 4, dtype=torch.int64, device=dev)
+trace = torch.zeros(nt * 4 + N * 8, dtype=torch.int64, device=dev)
 os.environ["GPFIT_PP_TRACE_PTR"] = str(trace.data_ptr())
 from gladsgp_amd import kernels
 X = torch.as_tensor(np.random.default_rng(0).random((n, 8)), device=dev)
@@ -44,29 +52,31 @@ for r in range(3):
 ch.check()
 t = trace.cpu().numpy().astype(np.float64)
 tk = t[: nt * 4].reshape(nt, 4)
-cs = t[nt * 4:].reshape(N, 4)
+cs = t[nt * 4:].reshape(N, 8)
 t0 = cs[0, 0]
 us = lambda x: (x - t0) / 100.0   # 100 MHz -> us
-print(f"n={n} N={N} tasks={nt}  chain span {us(cs[N-1, 2]):.1f} us; last task end "
+print(f"n={n} N={N} tasks={nt}  chain end {us(cs[N-1, 4]):.1f} us; last task end "
       f"{us(tk[1:, 3].max()):.1f} us")
-print("chain per step (us): a=wait DP+SYRK+fill, b=factor+store, c=wait SP+gemm+store")
-for j in range(N):
-    a = (cs[j, 1] - cs[j, 0]) / 100
-    b = (cs[j, 2] - cs[j, 1]) / 100
-    c = (cs[j, 3] - cs[j, 2]) / 100 if j + 1 < N else 0
-    dp = [k for k, x in enumerate(tasks) if x[0] == "DP" and x[2] == j]
-    sp = [k for k, x in enumerate(tasks) if x[0] == "SP" and x[2] == j]
-    dpl = us(tk[dp[0], 3]) - us(cs[j, 0]) if dp else float("nan")
-    spl = us(tk[sp[0], 3]) - us(cs[j, 2]) if sp else float("nan")
-    if j % 4 == 0 or j > N - 5:
-        print(f"j={j:3d} start {us(cs[j,0]):8.1f}  a {a:6.1f}  b {b:6.1f}  c {c:6.1f}   "
-              f"DP ready {dpl:+7.1f}  SP ready {spl:+7.1f} (rel. to need)")
+ph = ["waitDP", "syrk+fill", "factor", "storeD", "waitSP", "ldP", "gemm+st", "->next"]
+acc = np.zeros(8)
+for j in range(N - 1):
+    d = [(cs[j, q + 1] - cs[j, q]) / 100 for q in range(7)] + [(cs[j + 1, 0] - cs[j, 7]) / 100]
+    acc += d
+    if j % 8 == 0 or j > N - 4:
+        print(f"j={j:3d} start {us(cs[j, 0]):8.1f} " + " ".join(f"{p}={x:5.1f}" for p, x in zip(ph, d)))
+print("chain mean per step: " + " ".join(f"{p}={x / (N - 1):5.1f}" for p, x in zip(ph, acc)))
 kinds = {}
+ep = {}
 for k in range(1, nt):
     kd = tasks[k][0]
     kinds.setdefault(kd, []).append((tk[k, 2] - tk[k, 1]) / 100)
+    ep.setdefault(kd, []).append((tk[k, 3] - tk[k, 2]) / 100)
 for kd, v in kinds.items():
-    print(f"{kd}: {len(v)} tasks, accumulate mean {np.mean(v):.1f} us max {np.max(v):.1f}")
+    nterm = [(x[2] if x[0] in ("L", "SP") else x[2] - 1 if x[0] == "DP" else x[1] - x[2] if x[0] == "X"
+              else 2 * x[2] if x[0] == "LB" else 2 * (x[1] - x[2])) for x in tasks[1:] if x[0] == kd]
+    print(f"{kd}: {len(v)} tasks, accumulate mean {np.mean(v):.1f} us max {np.max(v):.1f}, "
+          f"terms mean {np.mean(nterm):.1f} -> {np.sum(v) / max(1, np.sum(nterm)):.2f} us/term; "
+          f"epilogue mean {np.mean(ep[kd]):.1f} us; WG-time total {np.sum(v) + np.sum(ep[kd]):.0f} us")
 # occupancy: fraction of 255 workers inside a task (start..end) per 100 us bucket
 span = us(tk[1:, 3].max())
 edges = np.arange(0, span + 100, 100)
@@ -78,3 +88,18 @@ for k in range(1, nt):
         busy[bi] += max(0, min(s2, e + 100) - max(s0, e)) / 100
         accb[bi] += max(0, min(s2, e + 100) - max(s2 - (s2 - s1), e)) / 100
 print("workers in a task per 100 us bucket:", " ".join(f"{x:.0f}" for x in busy))
+# per tile row: when its last L and X tile finished (us), and the X column-0 chain
+rowsL, rowsX, col0 = {}, {}, {}
+for k in range(1, nt):
+    kd, i, j = tasks[k]
+    end = us(tk[k, 3])
+    rows = [2 * i, 2 * i + 1] if kd in ("LB", "XB") else [i]
+    for r in rows:
+        if kd in ("L", "LB"): rowsL[r] = max(rowsL.get(r, 0), end)
+        if kd in ("X", "XB"): rowsX[r] = max(rowsX.get(r, 0), end)
+    if kd == "X" and j == 0: col0[i] = end
+    if kd == "XB" and j == 0: col0[2 * i] = col0[2 * i + 1] = end
+print("row: L done / X done / X col0 done (us)")
+for r in range(0, N, 4):
+    print(f"  {r:3d}: {rowsL.get(r, float('nan')):8.1f} {rowsX.get(r, float('nan')):8.1f} "
+          f"{col0.get(r, float('nan')):8.1f}")
