@@ -28,7 +28,7 @@ for n in sorted(tot, key=lambda k: -tot[k]):
     print(f"  {n:28s} {cnt[n]:5d} launches {tot[n]:9.1f} us")
 tr = [r for r in seq if name(r) in ("trmm_reduce_kernel", "trmm_pair_kernel", "finalize_kernel", "trmv_kernel")]
 first_trmv = min(int(r["Start_Timestamp"]) for r in tr)
-last_fact = max(int(r["End_Timestamp"]) for r in seq if name(r).startswith("chol_"))
+last_fact = max(int(r["End_Timestamp"]) for r in seq if name(r).startswith(("chol_", "pp_")))
 last_cross = max(int(r["End_Timestamp"]) for r in seq if name(r).startswith("cross_"))
 print(f"  factorisation ends {(last_fact - t0) / 1e3:.1f} us, cross-covariance ends "
       f"{(last_cross - t0) / 1e3:.1f} us, prediction starts {(first_trmv - t0) / 1e3:.1f} us")
