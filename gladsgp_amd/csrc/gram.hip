@@ -50,41 +50,6 @@ GP_DEV void tile_of(const GramShape& g, int t, int& ti, int& tj) {
   }
 }
 
-// exp(-a) for a >= 0 (a weighted squared distance), ~19 VALU ops: Cody-Waite reduction by ln 2,
-// a degree-11 minimax polynomial for e^r (|r| <= ln2/2; the coefficients ocml's exp uses), and
-// ldexp.  Every polynomial step is fma(p, r, c) with c a wave-uniform constant (an SGPR or
-// literal operand), so no constant has to be re-materialised in a VGPR per call (ocml's fmac
-// form overwrites its constant registers: 22 extra v_mov per exp inside a loop).  a is clamped
-// to 1100 first: e^-1100 underflows to +0 through the ldexp, the only range check a
-// non-negative argument needs.  Accuracy: within 1 ulp of exp (the same reduction and
-// polynomial as ocml).
-// fma(p, r, c) with c wave-uniform, pinned to VOP3 v_fma_f64 with c in an SGPR pair (the
-// compiler otherwise keeps c in a VGPR and copies it before every v_fmac_f64).
-GP_DEV double fma_sc(double p, double r, double c) {
-  double o;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(p), "v"(r), "s"(c));
-  return o;
-}
-
-GP_DEV double exp_neg(double a) {
-  const double x = -fmin(a, 1100.0);
-  const double k = __builtin_rint(x * 0x1.71547652b82fep+0);              // x log2(e)
-  double r = fma(k, -0x1.62e42fefa39efp-1, x);                             // - k ln2 (hi)
-  r = fma(k, -0x1.abc9e3b39803fp-56, r);                                   // - k ln2 (lo)
-  double p = fma_sc(r, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
-  p = fma_sc(p, r, 0x1.71dee623fde64p-19);
-  p = fma_sc(p, r, 0x1.a01997c89e6b0p-16);
-  p = fma_sc(p, r, 0x1.a01a014761f6ep-13);
-  p = fma_sc(p, r, 0x1.6c16c1852b7b0p-10);
-  p = fma_sc(p, r, 0x1.1111111122322p-7);
-  p = fma_sc(p, r, 0x1.55555555502a1p-5);
-  p = fma_sc(p, r, 0x1.5555555555511p-3);
-  p = fma_sc(p, r, 0x1.000000000000bp-1);
-  p = fma(p, r, 1.0);
-  p = fma(p, r, 1.0);
-  return __builtin_ldexp(p, (int)k);
-}
-
 template <int D>
 __global__ __launch_bounds__(256) void ardse_kernel(
     const double* __restrict__ XA, int na, int ldxa,      // row points (output rows)

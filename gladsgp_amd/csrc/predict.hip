@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
     }
     // exp unconditionally, then select: padding rows / columns have finite (zeroed) inputs,
     // and a conditional exp costs an exec-mask branch around each call
-    const double v0 = sb * exp(-e0), v1 = sb * exp(-e1);
+    const double v0 = sb * exp_neg(e0), v1 = sb * exp_neg(e1);
     o[(long long)k * mc + c] = (col_ok && k < n) ? v0 : 0.0;
     o[(long long)(k + 1) * mc + c] = (col_ok && k + 1 < n) ? v1 : 0.0;
   }
