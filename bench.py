@@ -12,12 +12,16 @@ runs on the caller-owned context's CU-masked stream while the latency-bound Chol
 (``--serial``: no context, every kernel in order on one stream).  Inputs are HBM-resident
 before the timed region.
 
-Multi-GPU (single-output GP): *strong scaling* of the fixed m = 100k test points.
-Rank r predicts the contiguous block ``shard_range(100000, r, N)``; every rank factorises the
-same n x n Gram redundantly (no exchange: the factorisation is the Amdahl term), and each step
-ends with one gather of every rank's (mean, var) rows to rank 0 (RCCL over xGMI), inside the
-timed region.  value = 100k * K / max-over-ranks(time).  The weak-scaled form (every rank its
-own 100k points, no collective) is reported beside it as ``weak`` when N > 1.
+Multi-GPU (single-output GP): *strong scaling* of the fixed m = 100k test points
+over a stream of GPs.  The headline at N > 1 is a two-stage pipeline (``c3_pipelined``): in step k
+rank 0 builds GP k+1's Gram and L, L^-1 and broadcasts L^-1 (RCCL, async, double-buffered)
+while every rank predicts GP k on its block of the test points, and each step ends with one
+gather of the (mean, var) blocks to rank 0 (inside the timed region).  Rank 0's block is
+shortened by the factorisation's measured time, consecutive GPs have different
+hyperparameters, and the last step is checked against a direct computation.  Beside it
+(``unpipelined``): every rank factorises the same Gram redundantly (the Amdahl term) and
+predicts ``shard_range(100000, r, N)``; and ``weak``: every rank its own 100k points.
+value = 100k * K / max-over-ranks(time).
 
 ``--workload c4`` runs BASELINE config 4 instead (multivariate emulator: 32 independent PC
 GPs, n = 1024, m = 100k shared test points): rank 0 broadcasts the inputs over RCCL at
@@ -152,6 +156,127 @@ def read_prof(pid):
     return cnt.value, max(tot.value, 1e-9)   # events off (GPFIT_BENCH_NOEVENTS=1): no data
 
 
+def c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed):
+    """N > 1: a two-stage pipeline over a stream of GPs ("rank 0 factorises and
+    broadcasts L").  GP k has hyperparameters beta (1 + 1e-3 (k mod 2)), so consecutive steps
+    are different GPs.  In step k rank 0 builds GP k+1's Gram and L, L^-1 (the persistent
+    factorisation) and broadcasts L^-1 over RCCL (async, into the other buffer of a
+    double-buffered pair), while every rank predicts GP k on its block of the 100k test points
+    and the (mean, var) blocks are gathered to rank 0.  Rank 0's block is shortened by the
+    factorisation's time in test-point equivalents (measured here: t_fact / t_point), so the
+    ranks finish together.  Every step still does one full Gram + factorisation and one full
+    100k-point prediction; a GP's latency is two steps.
+    Returns the timing, the split and a check of the last step against a direct single-rank
+    computation of the same GP on rank 0."""
+    import torch.distributed as dist
+    dev = ctx.device
+    N, rank = ctx.world, ctx.rank
+    n, d = X.shape
+    m = Xs.shape[0]
+    npad = kernels.padded_n(n)
+    Xd = torch.as_tensor(X, device=dev)
+    yd = torch.as_tensor(y, device=dev).reshape(1, n)
+    sd = torch.tensor([s], dtype=torch.float64, device=dev)
+    dd = torch.tensor([delta], dtype=torch.float64, device=dev)
+    betas = [torch.as_tensor(beta * (1.0 + 1e-3 * j), device=dev).reshape(1, d) for j in (0, 1)]
+    linv = [torch.zeros((1, npad, npad), dtype=torch.float64, device=dev) for _ in range(2)]
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    logdet = torch.zeros(1, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def factor(k):                      # rank 0: GP k's Gram -> L, L^-1 into linv[k % 2]
+        G = kernels.gram(Xd, betas[k % 2], sd, dd)
+        _capi.call("gp_potrf_inv", G.data_ptr(), n, n, n * n, linv[k % 2].data_ptr(), npad,
+                   npad * npad, 1, info.data_ptr(), logdet.data_ptr(), stream)
+
+    # calibration on rank 0: factorisation time and per-point prediction time
+    calib = torch.zeros(2, dtype=torch.float64, device=dev)
+    if rank == 0:
+        mc = min(m, 16384)
+        Xc = torch.as_tensor(Xs[:mc], device=dev).contiguous()
+        ch = kernels.Cholesky(n, None, linv[0], info, logdet)
+        tf, tp = [], []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            factor(0)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            kernels.predict(ch, Xd, Xc, betas[0], sd, sd, yd)
+            torch.cuda.synchronize()
+            tf.append(t1 - t0)
+            tp.append((time.perf_counter() - t1) / mc)
+        calib[0], calib[1] = sorted(tf)[1], sorted(tp)[1]
+        del Xc
+    gdist.broadcast_(ctx, calib)
+    t_fact, t_point = float(calib[0]), float(calib[1])
+    e = t_fact / t_point                # the factorisation in test-point equivalents
+    m1 = int(np.ceil((m + e) / N))
+    m0 = max(0, m - (N - 1) * m1)
+    rest = [gdist.shard_range(m - m0, r, N - 1) for r in range(N - 1)]
+    counts = [m0] + [b - a for a, b in rest]
+    lo = 0 if rank == 0 else m0 + rest[rank - 1][0]
+    ml = counts[rank]
+    Xsd = torch.as_tensor(Xs[lo:lo + ml], device=dev).contiguous()
+    out = torch.empty((2, max(ml, 1)), dtype=torch.float64, device=dev)
+    ws = kernels.PredictWorkspace()
+    chs = [kernels.Cholesky(n, None, linv[j], info, logdet) for j in (0, 1)]
+    state = {"k": 0, "pending": None, "res": None}
+
+    if ctx.backend == "nccl":
+        def bcast(k):                   # async on RCCL's stream, overlapping the prediction
+            return dist.broadcast(linv[k % 2], src=0, async_op=True)
+    else:
+        def bcast(k):                   # gloo (the 1-GPU tests): host-staged and synchronous
+            gdist.broadcast_(ctx, linv[k % 2])
+            return None
+
+    # prologue: GP 0 factorised and broadcast
+    if rank == 0:
+        factor(0)
+    state["pending"] = bcast(0)
+
+    def pipe_step():
+        k = state["k"]
+        if rank == 0:
+            factor(k + 1)
+        nxt = bcast(k + 1)
+        if state["pending"] is not None:
+            state["pending"].wait()
+        if ml:
+            kernels.predict(chs[k % 2], Xd, Xsd, betas[k % 2], sd, sd, yd, m_chunk=args.m_chunk,
+                            workspace=ws, out=(out[0:1, :ml], out[1:2, :ml]))
+        state["res"] = gdist.gather_cols(ctx, out[:, :ml], counts)
+        state["pending"] = nxt
+        state["k"] = k + 1
+
+    for _ in range(args.warmup):
+        pipe_step()
+    torch.cuda.synchronize()
+    elapsed = timed(pipe_step, args.steps)
+    if state["pending"] is not None:
+        state["pending"].wait()
+    torch.cuda.synchronize()
+    check = None
+    if rank == 0:
+        # the last step predicted GP k_last = state["k"] - 1: recompute it directly on a sample
+        k_last = state["k"] - 1
+        ns = min(2000, m)
+        G = kernels.gram(Xd, betas[k_last % 2], sd, dd)
+        ch = kernels.cholesky_inverse(G)
+        ch.check()
+        mu, var = kernels.predict(ch, Xd, torch.as_tensor(Xs[:ns], device=dev), betas[k_last % 2],
+                                  sd, sd, yd)
+        res = state["res"]
+        dm = float((res[0, :ns] - mu[0]).abs().max())
+        dv = float((res[1, :ns] - var[0]).abs().max())
+        check = {"gp": k_last, "points": ns, "max_abs_dmean": dm, "max_abs_dvar": dv}
+        if not (dm <= 1e-10 * max(1.0, float(mu.abs().max())) and dv <= 1e-12):
+            raise RuntimeError(f"pipelined result differs from the direct computation: {check}")
+    return {"elapsed": elapsed, "counts": counts, "t_fact_ms": t_fact * 1e3,
+            "t_point_us": t_point * 1e6, "check": check}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,6 +290,10 @@ def main():
                     help="test points the CPU baseline predicts per run (median of 3 runs)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling leg (N > 1)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="testing only: every rank on cuda:0 over gloo (host-staged collectives)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N > 1: headline = the redundant-factorisation strong split only")
     ap.add_argument("--workload", choices=("c3", "c4", "fit"), default="c3")
     ap.add_argument("--ny", type=int, default=1347945, help="fit: field size per run")
     ap.add_argument("--fit-pcs", type=int, default=8, help="fit: principal components")
@@ -186,7 +315,8 @@ def main():
     if args.workload == "fit":
         return main_fit(args)
 
-    ctx = gdist.init_from_env("cuda")
+    ctx = (gdist.init_from_env("cuda", backend="gloo", device_index=0) if args.share_gpu
+           else gdist.init_from_env("cuda"))
     dev = ctx.device
     n, m, d = args.n, args.m, args.d
     X, y, beta, Xs, s, delta = c3_inputs(n, m, d)
@@ -258,6 +388,9 @@ def main():
     res = gathered[0]
     if fctx is not None:
         fctx.close()
+    pipe = None
+    if ctx.world > 1 and not args.no_pipeline:
+        pipe = c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed)
     if ctx.rank != 0:
         return
     K = args.steps
@@ -326,6 +459,26 @@ def main():
     }
     if res is None or tuple(res.shape) != (2, m):
         raise RuntimeError(f"gathered result has shape {None if res is None else res.shape}")
+    if pipe is not None:
+        # the pipelined schedule is the headline at N > 1; the redundant-factorisation strong
+        # split stays beside it
+        line["unpipelined"] = {"value": value, "unit": "predictions/s",
+                               "ms_per_step": elapsed / K * 1e3,
+                               "parallelism": line["config"]["parallelism"]}
+        line["value"] = m * K / pipe["elapsed"]
+        line["ms_per_step"] = pipe["elapsed"] / K * 1e3
+        line["config"]["parallelism"] = (
+            f"pipelined x{ctx.world}: rank 0 builds GP k+1's Gram + L, L^-1 and broadcasts L^-1 "
+            "(RCCL, async, double-buffered) while every rank predicts GP k on its test-point "
+            "block and the blocks are gathered to rank 0; rank 0's block shortened by the "
+            "factorisation's time")
+        line["config"]["m_test_per_rank"] = pipe["counts"]
+        line["config"]["m_test_rank0"] = pipe["counts"][0]
+        line["config"]["pipeline"] = ("per rank: gp_predict (cross-covariance, TRMM, mean/var) "
+                                      "from the broadcast L^-1; rank 0 also gp_gram_ardse + "
+                                      "gp_potrf_inv of the next GP, first")
+        line["pipeline"] = {"t_fact_ms": pipe["t_fact_ms"], "t_point_us": pipe["t_point_us"],
+                            "check_last_step_vs_direct": pipe["check"]}
     if ctx.world == 1 and not args.no_cpu:
         cb, mu_ref, var_ref = cpu_baseline(X, y, beta, Xs, s, delta, args.cpu_sample)
         k = mu_ref.shape[0]
