@@ -130,7 +130,7 @@ def _pipe_worker(rank, world, port, results):
     from gladsgp_amd import dist as gdist
     ctx = gdist.init_from_env("cuda", backend="gloo", device_index=0)
     try:
-        X, y, beta, Xs, s, delta = bench.c3_inputs(640, 3000, 8)
+        X, y, beta, Xs, s, delta = bench.c3_inputs(640, 40000, 8)
         args = types.SimpleNamespace(warmup=2, steps=3, m_chunk=0)
 
         def timed(fn, steps):
@@ -164,6 +164,6 @@ def test_two_ranks_pipelined_c3():
         res = dict(results[r])
         assert "error" not in res, res.get("error")
     counts = results[0]["counts"]
-    assert sum(counts) == 3000 and len(counts) == 2 and 0 < counts[0] <= counts[1]
+    assert sum(counts) == 40000 and len(counts) == 2 and 0 < counts[0] <= counts[1]
     chk = results[0]["check"]
     assert chk["gp"] == 4 and chk["max_abs_dmean"] <= 1e-12 and chk["max_abs_dvar"] <= 1e-12, chk
