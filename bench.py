@@ -14,7 +14,7 @@ before the timed region.
 
 Multi-GPU (single-output GP): *strong scaling* of the fixed m = 100k test points
 over a stream of GPs.  The headline at N > 1 is a two-stage pipeline (``c3_pipelined``): in step k
-rank 0 builds GP k+1's Gram and L, L^-1 and broadcasts L^-1 (RCCL, async, double-buffered)
+rank 0 builds GP k+1's Gram and L, L^-1 and broadcasts L^-1 (RCCL, async, packed to the lower triangle, double-buffered)
 while every rank predicts GP k on its block of the test points, and each step ends with one
 gather of the (mean, var) blocks to rank 0 (inside the timed region).  Rank 0's block is
 shortened by the factorisation's measured time, consecutive GPs have different
@@ -170,7 +170,7 @@ def c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed):
     """N > 1: a two-stage pipeline over a stream of GPs ("rank 0 factorises and
     broadcasts L").  GP k has hyperparameters beta (1 + 1e-3 (k mod 2)), so consecutive steps
     are different GPs.  In step k rank 0 builds GP k+1's Gram and L, L^-1 (the persistent
-    factorisation) and broadcasts L^-1 over RCCL (async, into the other buffer of a
+    factorisation) and broadcasts L^-1 over RCCL (async, its lower triangle packed, into the other buffer of a
     double-buffered pair), while every rank predicts GP k on its block of the 100k test points
     and the (mean, var) blocks are gathered to rank 0.  Rank 0's block is shortened by the
     factorisation's time in test-point equivalents (measured here: t_fact / t_point), so the
@@ -231,12 +231,24 @@ def c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed):
     chs = [kernels.Cholesky(n, None, linv[j], info, logdet) for j in (0, 1)]
     state = {"k": 0, "pending": None, "res": None}
 
+    # L^-1 travels packed: its nonzero part, column c (col-major) from row c on, half the bytes
+    # of the padded square.  Rank 0 gathers it after the factorisation; the others scatter it
+    # into receive buffers that were zero-filled once (the upper triangle never changes).
+    tri = torch.triu_indices(npad, npad, device=dev)     # (c, r), r >= c, of the [c][r] view
+    flat = tri[0] * npad + tri[1]
+    del tri
+    packed = [torch.empty(flat.numel(), dtype=torch.float64, device=dev) for _ in range(2)]
+
     if ctx.backend == "nccl":
         def bcast(k):                   # async on RCCL's stream, overlapping the prediction
-            return dist.broadcast(linv[k % 2], src=0, async_op=True)
+            if rank == 0:
+                torch.index_select(linv[k % 2].view(-1), 0, flat, out=packed[k % 2])
+            return dist.broadcast(packed[k % 2], src=0, async_op=True)
     else:
         def bcast(k):                   # gloo (the 1-GPU tests): host-staged and synchronous
-            gdist.broadcast_(ctx, linv[k % 2])
+            if rank == 0:
+                torch.index_select(linv[k % 2].view(-1), 0, flat, out=packed[k % 2])
+            gdist.broadcast_(ctx, packed[k % 2])
             return None
 
     # prologue: GP 0 factorised and broadcast
@@ -251,6 +263,8 @@ def c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed):
         nxt = bcast(k + 1)
         if state["pending"] is not None:
             state["pending"].wait()
+        if rank != 0:                   # GP k's L^-1 from its packed broadcast
+            linv[k % 2].view(-1).index_copy_(0, flat, packed[k % 2])
         if ml:
             kernels.predict(chs[k % 2], Xd, Xsd, betas[k % 2], sd, sd, yd, m_chunk=args.m_chunk,
                             workspace=ws, out=(out[0:1, :ml], out[1:2, :ml]))
@@ -477,7 +491,7 @@ def main():
         line["ms_per_step"] = pipe["elapsed"] / K * 1e3
         line["config"]["parallelism"] = (
             f"pipelined x{ctx.world}: rank 0 builds GP k+1's Gram + L, L^-1 and broadcasts L^-1 "
-            "(RCCL, async, double-buffered) while every rank predicts GP k on its test-point "
+            "(RCCL, async, packed to the lower triangle, double-buffered) while every rank predicts GP k on its test-point "
             "block and the blocks are gathered to rank 0; rank 0's block shortened by the "
             "factorisation's time")
         line["config"]["m_test_per_rank"] = pipe["counts"]
