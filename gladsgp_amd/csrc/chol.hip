@@ -900,12 +900,13 @@ __global__ void trtri_info_kernel(int* __restrict__ info, int batch) {
 // byte with sc1 loads.  Every wait also watches the problem's abort word (non-PD pivot) and a
 // poll budget, so no path can spin forever.
 // ------------------------------------------------------------------------------------------
-constexpr int kPPMaxN = 250;          // schedule_kernel: one thread per key (4N+23 <= 1024)
+constexpr int kPPMaxN = 240;          // schedule_kernel: one thread per key (4N+63 <= 1024)
 constexpr int kTChain = 0, kTL = 1, kTDP = 2, kTSP = 3, kTX = 4;
 constexpr long long kPollBudget = 1ll << 22;   // s_sleep polls before a wait gives up
 
 __shared__ double g_keep[NB * LP];    // chain: L_j+1,j as [p][r] (opA layout) between steps
 __shared__ int g_msg[4];              // dequeued task / wait results broadcast to the workgroup
+__shared__ long long g_stall;         // debug trace only: ticks thread 0 spent polling flags
 
 struct PPArgs {
   double* A; long long sA; int lda;
@@ -948,17 +949,26 @@ typedef unsigned int pp_u4 __attribute__((ext_vector_type(4)));
 
 // Tile load into registers (load_op's slot map) with sc1 loads: 16-B buffer loads for a full,
 // aligned tile, else bounds-checked 8-B loads (zero outside fv x sv).
-GP_DEV void pp_load(OpTile& t, const double* src, int ld, int fv, int sv) {
+GP_DEV void pp_load(OpTile& t, const double* src, int ld, int fv, int sv, bool coh = true) {
   const int tid = threadIdx.x;
   const bool full = fv == NB && sv == NB && (ld & 1) == 0 && (((size_t)src & 15) == 0);
   if (full) {
     const __amdgpu_buffer_rsrc_t r = pp_rsrc(src);
     const int base = ((tid & 31) * 2 + (tid >> 5) * ld) * 8;
+    pp_u4 x[8];
+    if (coh) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        x[q] = __builtin_amdgcn_raw_buffer_load_b128(r, base + q * 64 * ld, 0, 16);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        x[q] = __builtin_amdgcn_raw_buffer_load_b128(r, base + q * 64 * ld, 0, 0);
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const pp_u4 x = __builtin_amdgcn_raw_buffer_load_b128(r, base + q * 64 * ld, 0, 16);
-      t.v[2 * q] = __longlong_as_double(((long long)x.y << 32) | x.x);
-      t.v[2 * q + 1] = __longlong_as_double(((long long)x.w << 32) | x.z);
+      t.v[2 * q] = __longlong_as_double(((long long)x[q].y << 32) | x[q].x);
+      t.v[2 * q + 1] = __longlong_as_double(((long long)x[q].w << 32) | x[q].z);
     }
   } else {
 #pragma unroll
@@ -1085,11 +1095,13 @@ GP_DEV void acc_to_lds_rm(double* Cs, const f64x4 (&acc)[2][2]) {
 GP_DEV bool pp_wait1(const int* f, int* abort) {
   if (threadIdx.x == 0) {
     int ok = 0;
+    const long long ts = pp_now();
     for (long long it = 0; it < kPollBudget; ++it) {
       if (pp_ldflag(f)) { ok = 1; break; }
       if (pp_ldflag(abort)) break;
       __builtin_amdgcn_s_sleep(2);
     }
+    g_stall += pp_now() - ts;
     if (!ok && !pp_ldflag(abort)) pp_stflag(abort, 2);   // budget spent: give up the problem
     g_msg[1] = ok;
   }
@@ -1114,6 +1126,7 @@ struct PPTerm {
   const int *fa, *fb;
   int lda_, ldb_, av, bv;   // av: valid rows of opA's tile; bv: valid rows of opB's (NAT)
   bool btrn;
+  bool ca, cb;              // operand tile rewritten in place during the launch: sc1 load
 };
 
 struct PPTask {
@@ -1131,15 +1144,21 @@ GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
   u.lda_ = P.lda;
   u.ldb_ = P.lda;
   u.btrn = false;
+  // L tiles (r, k) with r - k <= 1 pass through P partial sums in place (DP / SP tasks on any
+  // XCD) before the chain writes L: read them with sc1 so no XCD's L2 serves a stale line.  Every
+  // other operand tile is written once, by the XCD that alone read its old contents, and is
+  // only read after its flag: plain loads, cached in each reader's L2.
+  auto hz = [&](int r, int k) { return r - k <= 1; };
   if (T.kind == kTL || T.kind == kTSP) {   // L_ik L_jk^T with (i, j) = (T.i, T.j)
-    u.a = atile(T.i, t);  u.fa = F + T.i * N + t;  u.av = rv(T.i);
-    u.b = atile(T.j, t);  u.fb = F + T.j * N + t;  u.bv = rv(T.j);
+    u.a = atile(T.i, t);  u.fa = F + T.i * N + t;  u.av = rv(T.i);  u.ca = hz(T.i, t);
+    u.b = atile(T.j, t);  u.fb = F + T.j * N + t;  u.bv = rv(T.j);  u.cb = hz(T.j, t);
   } else if (T.kind == kTDP) {             // L_jk L_jk^T
-    u.a = atile(T.j, t);  u.fa = F + T.j * N + t;  u.av = rv(T.j);
-    u.b = u.a;            u.fb = u.fa;             u.bv = u.av;
+    u.a = atile(T.j, t);  u.fa = F + T.j * N + t;  u.av = rv(T.j);  u.ca = hz(T.j, t);
+    u.b = u.a;            u.fb = u.fa;             u.bv = u.av;     u.cb = u.ca;
   } else {                                 // XT: L_ik X_kc, k = c + t (X_cc = D_c)
     const int k = T.j + t;
-    u.a = atile(T.i, k);  u.fa = F + T.i * N + k;  u.av = rv(T.i);
+    u.a = atile(T.i, k);  u.fa = F + T.i * N + k;  u.av = rv(T.i);  u.ca = hz(T.i, k);
+    u.cb = false;
     u.b = Xb + k * NB + (long long)T.j * NB * P.ldx;
     u.ldb_ = P.ldx;
     u.fb = (k == T.j) ? F + k * N + k : F + N * N + k * N + T.j;
@@ -1155,6 +1174,7 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     int res = -1;
+    const long long ts = pp_now();
     for (long long it = 0; it < kPollBudget; ++it) {
       const int t = t0 + lane;
       bool rdy = true;
@@ -1171,6 +1191,7 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
     }
     if (res < 0 && lane == 0 && !pp_ldflag(abort)) pp_stflag(abort, 2);
     if (lane == 0) g_msg[2] = res;
+    if (lane == 0) g_stall += pp_now() - ts;
   }
   __syncthreads();
   const int r = g_msg[2];
@@ -1179,8 +1200,8 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
 }
 
 GP_DEV void pp_load_term(const PPTerm& u, OpTile& ta, OpTile& tb) {
-  pp_load(ta, u.a, u.lda_, u.av, NB);
-  if (u.b != u.a) pp_load(tb, u.b, u.ldb_, u.bv, NB);
+  pp_load(ta, u.a, u.lda_, u.av, NB, u.ca);
+  if (u.b != u.a) pp_load(tb, u.b, u.ldb_, u.bv, NB, u.cb);
 }
 
 // Worker: accumulate the task's K steps in registers (software-pipelined: the next step's
@@ -1264,11 +1285,13 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   double* Ab = P.A + T.b * P.sA;
   f64x4 acc[2][2];
   PP_MARK(P, 20 + T.kind, T.i * 1000 + T.j);
-  PP_TRACE(P, (long long)T.idx * 4 + 0, blockIdx.x);
+  if (threadIdx.x == 0) g_stall = 0;
   PP_TRACE(P, (long long)T.idx * 4 + 1, pp_now());
   if (!pp_accumulate(P, T, acc, abort)) return;
   PP_MARK(P, 30 + T.kind, T.i * 1000 + T.j);
   PP_TRACE(P, (long long)T.idx * 4 + 2, pp_now());
+  // slot 0: workgroup | ticks polled before the K loop finished << 8
+  PP_TRACE(P, (long long)T.idx * 4 + 0, blockIdx.x | (g_stall << 8));
   auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
   auto rv = [&](int r) { return min(NB, P.n - r * NB); };
   if (T.kind == kTDP || T.kind == kTSP) {
@@ -1462,10 +1485,16 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
   }
 }
 
-// Task list: batch chain entries, then per key t = 0..4N-2+4W (anti-diagonal order, see the
-// section comment) the tasks of that key, each for every problem:
+// Task list: batch chain entries, then per key t = 0..4N-2+4(W+XD) (anti-diagonal order, see
+// the section comment) the tasks of that key, each for every problem:
 //   DP(j): t = 4j-2;  SP(j): t = 4j+1;  band LT(i,j), i-j <= kPPBand: t = 2(i+j)   ("early")
-//   other LT(i,j): t = 2(i+j) + 4W;  XT(i,c): t = 4i+2 + 4W
+//   other LT(i,j): t = 2(i+j) + 4W;  XT(i,c): t = 4i+2 + 4(W+XD), c = 0 first
+// XT tasks wait on whole rows of L (their last K step on L_i,i-1, a chain output): dequeued
+// with the LT tasks (XD = 0) they sat polling in ~25% of the workers while the LT / SP tasks the
+// chain waits on queued behind them (pp_trace: 145 ms of 588 ms worker time polling, the
+// chain waiting 7-26 us per step for SP from step ~36 on); XD = kPPXDelay = 8 leaves those
+// workers to the LT tasks (n = 4096: 2.12-2.17 vs 2.44-2.46 ms, profiles/r02/ab_pp_xt_delay.log).
+// Emitting each row's longest XT (c = 0) first shortens the tail after the chain.
 // The early tasks are what the chain waits on (its partials and the near-diagonal tiles the
 // partials wait on): they are dequeued kPPLead = W chain steps ahead of their topological
 // position, early enough to catch up on their K steps that are already available.  Only
@@ -1478,14 +1507,15 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
 constexpr int kPPLead = 6;
 constexpr int kPPLeadBlocked = 4 * kPPLead + 2;   // per-problem bound on blocked early tasks
 constexpr int kPPBand = 3;
+constexpr int kPPXDelay = 8;   // XT tasks: 8 chain steps after the late LT tasks of their row
 
 // The tasks of key t in emission order (f(kind, i, j) per task; see pp_schedule_kernel):
 //   early  DP(j): t = 4j-2;  SP(j): t = 4j+1;  band LT(i,j), 2 <= i-j <= kPPBand: t = 2(i+j)
-//   late   (K = t - 4W)  XT(i,c): K = 4i+2;  LT(i,j), i-j > kPPBand: K = 2(i+j)
+//   late   (K = t - 4W)  XT(i,c): K = 4i+2 + 4XD;  LT(i,j), i-j > kPPBand: K = 2(i+j)
 // Every input of a late task has a smaller key or is a chain step whose own inputs do (see the
 // section comment).  Shared by the schedule kernel (count + emit) and the host's task count.
 template <typename F>
-GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, F&& f) {
+GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, int xd, F&& f) {
   if (t % 4 == 2 && (t + 2) / 4 >= 2 && (t + 2) / 4 <= N - 1) f(kTDP, 0, (t + 2) / 4);
   if (t % 4 == 1 && (t - 1) / 4 >= 1 && (t - 1) / 4 <= N - 2) f(kTSP, (t - 1) / 4 + 1, (t - 1) / 4);
   if (t % 2 == 0 && t >= 4) {                                  // band LT on anti-diagonal s
@@ -1495,9 +1525,10 @@ GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, F&& f) {
   }
   const int K = t - 4 * lead;
   if (K < 0) return;
-  if (inv && K % 4 == 2 && (K - 2) / 4 >= 1 && (K - 2) / 4 <= N - 1) {
-    const int i = (K - 2) / 4;
-    for (int c = i - 1; c >= 0; --c) f(kTX, i, c);             // nearest the diagonal first
+  const int KX = K - 4 * xd;
+  if (inv && KX >= 0 && KX % 4 == 2 && (KX - 2) / 4 >= 1 && (KX - 2) / 4 <= N - 1) {
+    const int i = (KX - 2) / 4;
+    for (int c = 0; c < i; ++c) f(kTX, i, c);                  // longest (most K steps) first
   }
   if (K % 2 == 0) {                                            // late LT singles
     const int s = K / 2;
@@ -1506,15 +1537,15 @@ GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, F&& f) {
   }
 }
 
-GP_HD inline int pp_nkeys(int N, int lead) { return 4 * N - 1 + 4 * lead; }
+GP_HD inline int pp_nkeys(int N, int lead, int xd) { return 4 * N - 1 + 4 * (lead + xd); }
 
 __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, int batch,
-                                                           int inv, int lead) {
+                                                           int inv, int lead, int xd) {
   __shared__ int cnt[2][1024];
   const int T = threadIdx.x;
-  const int nk = pp_nkeys(N, lead);
+  const int nk = pp_nkeys(N, lead, xd);
   int own = 0;
-  if (T < nk) pp_for_key(T, N, inv != 0, lead, [&](int, int, int) { ++own; });
+  if (T < nk) pp_for_key(T, N, inv != 0, lead, xd, [&](int, int, int) { ++own; });
   cnt[0][T] = own;
   __syncthreads();
   int src = 0;
@@ -1527,7 +1558,7 @@ __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, i
   if (T >= nk) return;
   const int excl = cnt[src][T] - own;
   long long pos = batch + (long long)excl * batch;
-  pp_for_key(T, N, inv != 0, lead, [&](int kind, int i, int j) {
+  pp_for_key(T, N, inv != 0, lead, xd, [&](int kind, int i, int j) {
     for (int b = 0; b < batch; ++b) tasks[pos++] = make_int2(kind | (b << 4), i | (j << 16));
   });
 }
@@ -1536,7 +1567,8 @@ __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, i
 // same total).
 long long pp_task_count(int N, bool inv) {
   long long c = 1;
-  for (int t = 0; t < pp_nkeys(N, 0); ++t) pp_for_key(t, N, inv, 0, [&](int, int, int) { ++c; });
+  for (int t = 0; t < pp_nkeys(N, 0, 0); ++t)
+    pp_for_key(t, N, inv, 0, 0, [&](int, int, int) { ++c; });
   return c;
 }
 
@@ -1631,7 +1663,7 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   int* flags = reinterpret_cast<int*>(scr + task_bytes + 256);
   const int lead = pp_lead(batch, grid);
   hipLaunchKernelGGL(pp_schedule_kernel, dim3(1), dim3(1024), 0, stream, tasks, N, batch,
-                     inv ? 1 : 0, lead);
+                     inv ? 1 : 0, lead, kPPXDelay);
   GP_CK(hipGetLastError());
   PPArgs P;
   P.A = A; P.sA = sA; P.lda = lda;

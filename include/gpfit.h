@@ -303,7 +303,7 @@ int gp_gather(void* comm, const void* send, long long bytes, void* recv, int roo
  */
 #define GP_PROF_GRAM 0        /* gram / cross-covariance build (ardse_kernel)            */
 #define GP_PROF_POTRF 1       /* whole gp_potrf_inv sequence                             */
-#define GP_PROF_TRMM 2        /* predict: trmm_reduce_kernel (dominant kernel)           */
+#define GP_PROF_TRMM 2        /* predict: trmm_pair_kernel (dominant kernel)             */
 #define GP_PROF_CROSS 3       /* predict: per-chunk cross-covariance build               */
 #define GP_PROF_NUM 4
 int gp_profile_enable(int capacity);

@@ -8,11 +8,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N = (n + 63) // 64
 W, B = 6, 3  # chol.hip kPPLead, kPPBand
+XD = 8      # chol.hip kPPXDelay
 NBf = 0   # no block tasks
 in_ltb = lambda i, j: (i >> 1) < NBf and (i >> 1) - (j >> 1) >= 3
 in_xtb = lambda i, c: (i >> 1) < NBf and (i >> 1) > (c >> 1)
 tasks = [("C", 0, 0)]
-for t in range(4 * N - 1 + 4 * W):          # chol.hip pp_for_key
+for t in range(4 * N - 1 + 4 * (W + XD)):          # chol.hip pp_for_key
     if t % 4 == 2 and 2 <= (t + 2) // 4 <= N - 1: tasks.append(("DP", 0, (t + 2) // 4))
     if t % 4 == 1 and 1 <= (t - 1) // 4 <= N - 2: tasks.append(("SP", (t - 1) // 4 + 1, (t - 1) // 4))
     if t % 2 == 0 and t >= 4:
@@ -21,9 +22,10 @@ for t in range(4 * N - 1 + 4 * W):          # chol.hip pp_for_key
         tasks += [("L", s_ - j, j) for j in range((s_ - 2) // 2, max(jmin, 0) - 1, -1)]
     K = t - 4 * W
     if K < 0: continue
-    if K % 4 == 2 and 1 <= (K - 2) // 4 <= N - 1:
-        i = (K - 2) // 4
-        tasks += [("X", i, c) for c in range(i - 1, -1, -1) if not in_xtb(i, c)]
+    KX = K - 4 * XD
+    if KX >= 0 and KX % 4 == 2 and 1 <= (KX - 2) // 4 <= N - 1:
+        i = (KX - 2) // 4
+        tasks += [("X", i, c) for c in range(i) if not in_xtb(i, c)]
     if K % 8 == 2 and 1 <= (K - 2) // 8 < NBf:
         I = (K - 2) // 8
         tasks += [("XB", I, C) for C in range(I - 1, -1, -1)]
@@ -67,16 +69,20 @@ for j in range(N - 1):
 print("chain mean per step: " + " ".join(f"{p}={x / (N - 1):5.1f}" for p, x in zip(ph, acc)))
 kinds = {}
 ep = {}
+stall = {}
 for k in range(1, nt):
     kd = tasks[k][0]
     kinds.setdefault(kd, []).append((tk[k, 2] - tk[k, 1]) / 100)
     ep.setdefault(kd, []).append((tk[k, 3] - tk[k, 2]) / 100)
+    stall.setdefault(kd, []).append((int(tk[k, 0]) >> 8) / 100)
 for kd, v in kinds.items():
     nterm = [(x[2] if x[0] in ("L", "SP") else x[2] - 1 if x[0] == "DP" else x[1] - x[2] if x[0] == "X"
               else 2 * x[2] if x[0] == "LB" else 2 * (x[1] - x[2])) for x in tasks[1:] if x[0] == kd]
     print(f"{kd}: {len(v)} tasks, accumulate mean {np.mean(v):.1f} us max {np.max(v):.1f}, "
           f"terms mean {np.mean(nterm):.1f} -> {np.sum(v) / max(1, np.sum(nterm)):.2f} us/term; "
-          f"epilogue mean {np.mean(ep[kd]):.1f} us; WG-time total {np.sum(v) + np.sum(ep[kd]):.0f} us")
+          f"epilogue mean {np.mean(ep[kd]):.1f} us; WG-time total {np.sum(v) + np.sum(ep[kd]):.0f} us; "
+          f"polling for inputs inside the K loop {np.sum(stall[kd]):.0f} us "
+          f"-> {(np.sum(v) - np.sum(stall[kd])) / max(1, np.sum(nterm)):.2f} us/term computing")
 # occupancy: fraction of 255 workers inside a task (start..end) per 100 us bucket
 span = us(tk[1:, 3].max())
 edges = np.arange(0, span + 100, 100)
