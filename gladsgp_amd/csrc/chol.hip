@@ -380,50 +380,58 @@ GP_DEV void st16(lds_double* Cb, const f64x4& a, double sg) {
 }
 
 // One wave: factor + invert the 16 x 16 block at (o, o).  Writes L_bb into T's block and
-// Dinv_b into U's block (lower, zero upper); returns the first failing pivot (1-based, tile
-// index) among rows < nb, or 0; adds sum log pivots (rows < nb) to lg.
-GP_DEV int leaf16(lds_double* T, lds_double* U, int o, int nb, double& lg) {
+// Dinv_b into U's block (lower, zero upper) and the 16 pivots p_c (L_cc = sqrt(p_c)) into
+// piv[o + c]; the caller checks them.
+//
+// The block lives in MFMA C layout (lane l, reg q = element [(l >> 4) + 4q][l & 15]), so row j
+// of the block is register j / 4 of lanes 16 (j % 4) .. + 15, which is at once the A operand's
+// column k = j % 4 (A[i][k] from lane 16k + i) and the B operand's row k (B[k][c] from lane
+// 16k + c).  Elimination step j is therefore ONE v_mfma_f64_16x16x4 on the whole block,
+//   A[i][c] -= A[j][i] (A[j][c] / p_j)    (i, c > j; the other three k lanes zero),
+// and one more applies the same row operation to W (= I at the start): W[i][c] -= m_i W[j][c],
+// m_i = A[j][i] / p_j.  Both factors come from row j only, the same copy for every row (the
+// rounding asymmetry of the trailing block never feeds back; see diag_factor_inv).  At the end
+// A's lower triangle holds Lt[r][c] p_c and W = Lt^-1:  L = A D^-1/2 (columns), L^-1 = D^-1/2 W
+// (rows).  Per step the dependent chain is readlane -> rcp + 2 Newton -> select -> MFMA; the
+// register-resident form with one readlane pair per row and step (and the SGPR traffic that
+// came with it) measured 8.5k cycles per leaf (tools/dbg/leaf_micro.hip).
+GP_DEV void leaf16(lds_double* T, lds_double* U, int o, lds_double* piv) {
   const int lane = threadIdx.x & 63;
-  const int c = lane & 15;
-  const bool fac = lane < 16;
-  double v[16];
+  const int r0 = lane >> 4, c = lane & 15;
+  f64x4 A = ld16(T + o * LP + o);
+  f64x4 W;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = fac ? T[(o + r) * LP + o + c] : (r == c ? 1.0 : 0.0);
-  double rsq[16];
-  double mypiv = 1.0;
+  for (int q = 0; q < 4; ++q) W[q] = (r0 + 4 * q == c) ? 1.0 : 0.0;
+  double colpiv = 1.0;          // p_c of this lane's column
+  double rowpiv[4];             // p_r of rows r0 + 4q
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rowpiv[q] = 1.0;
   static_for<0, 16, 1>([&](auto J) {
     constexpr int j = decltype(J)::value;
-    const double p = readlane_f64(v[j], j);
-    mypiv = (c == j) ? p : mypiv;
-    const double rp = rcp_nr(p);
-    // factor lanes: t_c = A[j][c] / p for c > j (columns <= j are final); inverse lanes:
-    // B[j][c] / p.  Row r's factor A[r][j] is lane r's own row-j value (the upper copy).
-    const double y = (fac && c <= j) ? 0.0 : v[j] * rp;
-    static_for<j + 1, 16, 1>([&](auto R) {
-      constexpr int r = decltype(R)::value;
-      v[r] = fma(-readlane_f64(v[j], r), y, v[r]);
-    });
-    rsq[j] = p;
-  });
-#pragma unroll
-  for (int r = 0; r < 16; ++r) rsq[r] = rsqrt_nr(rsq[r]);
-  const double myrs = rsqrt_nr(mypiv);
-  if (lane < 32) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (fac)
-        T[(o + r) * LP + o + c] = r > c ? v[r] * myrs : (r == c ? mypiv * myrs : 0.0);
-      else
-        U[(o + r) * LP + o + c] = r >= c ? v[r] * rsq[r] : 0.0;
+    constexpr int q = j >> 2, k = j & 3;
+    const double p = readlane_f64(A[q], 16 * k + j);
+    colpiv = (c == j) ? p : colpiv;
+    rowpiv[q] = (r0 == k) ? p : rowpiv[q];
+    if constexpr (j < 15) {
+      const double rp = rcp_nr(p);
+      const bool sel = r0 == k && c > j;
+      const double rowj = A[q];
+      const double a = sel ? -rowj : 0.0;
+      const double m = sel ? rowj * rp : 0.0;
+      const double wj = W[q];
+      A = mfma16x16x4(a, m, A);
+      W = mfma16x16x4(-m, wj, W);
     }
-  }
-  const bool ok = !(lane < 16 && o + c < nb) || (mypiv > 0.0 && isfinite(mypiv));
-  const unsigned long long bad = __ballot(!ok);
-  double l = (lane < 16 && o + c < nb) ? log(mypiv) : 0.0;
+  });
+  const double rsc = rsqrt_nr(colpiv);
 #pragma unroll
-  for (int off = 8; off > 0; off >>= 1) l += __shfl_xor(l, off, 64);
-  lg += readlane_f64(l, 0);
-  return bad ? o + __ffsll((long long)bad) : 0;
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + 4 * q;
+    const double rsr = rsqrt_nr(rowpiv[q]);
+    T[(o + r) * LP + o + c] = r >= c ? A[q] * rsc : 0.0;
+    U[(o + r) * LP + o + c] = r >= c ? W[q] * rsr : 0.0;
+  }
+  if (lane < 16) piv[o + c] = colpiv;
 }
 
 GP_DEV int diag_factor_blk(int nb, double* ld_out) {
@@ -431,14 +439,10 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
   lds_double* T = sm.As;
   lds_double* U = sm.Bs;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int fail = 0;
-  double lg = 0.0;
+  lds_double* piv = sm.invs;
   static_for<0, 4, 1>([&](auto Bk) {
     constexpr int b = decltype(Bk)::value;
-    if (w == 0) {
-      const int f = leaf16(T, U, 16 * b, nb, lg);
-      if (!fail) fail = f;
-    }
+    if (w == 0) leaf16(T, U, 16 * b, piv);
     __syncthreads();
     if constexpr (b < 3) {
       // panel: L_rb = A_rb Dinv_b^T, r = b + w
@@ -466,7 +470,20 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
     }
   });
   // inverse: wave c builds column block c (X_cc = Dinv_c already in U); scratch = T's upper
-  // block (c, r)
+  // block (c, r).  Wave 3 meanwhile checks the 64 pivots and sums their logs.
+  if (w == 3) {
+    const int lane = threadIdx.x & 63;
+    const double p = piv[lane];
+    const bool bad = lane < nb && !(p > 0.0 && isfinite(p));
+    const unsigned long long badm = __ballot(bad);
+    double l = lane < nb ? log(p) : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) l += __shfl_xor(l, off, 64);
+    if (lane == 0) {
+      sm.fail = badm ? __ffsll((long long)badm) : 0;
+      sm.red[0] = l;
+    }
+  }
   if (w < 3) {
     const int c = w;
     for (int r = c + 1; r <= 3; ++r) {
@@ -489,10 +506,6 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
       T[r * LP + cc] = 0.0;
       U[r * LP + cc] = 0.0;
     }
-  }
-  if (threadIdx.x == 0) {
-    sm.fail = fail;
-    sm.red[0] = lg;
   }
   __syncthreads();
   const int f = sm.fail;
