@@ -1260,21 +1260,24 @@ GP_DEV bool pp_accumulate(const PPArgs& P, const PPTask& T, f64x4 (&acc)[2][2], 
 }
 
 // C (As as [col][row]) = A tile - acc, for rows < rv / cols < cv (zero elsewhere).  lower:
-// only row >= col is read from A (diagonal tiles; the upper part of A is never read).
-GP_DEV void pp_sub_from_a(const double* src, int ld, int rv, int cv, bool lower,
-                          const f64x4 (&acc)[2][2]) {
+// only row >= col is taken from A (diagonal tiles; the upper part of A is never read).  The A
+// tile was loaded into registers (pp_load's slot map: column (tid >> 5) + 8q, rows
+// 2 (tid & 31) + {0, 1}) when the task started, so its latency hides under the K loop.
+GP_DEV void pp_sub_tile(const OpTile& a, int rv, int cv, bool lower, const f64x4 (&acc)[2][2]) {
   Smem& sm = g_sm;
+  const int tid = threadIdx.x;
   __syncthreads();
   acc_to_lds(sm.As, acc);
   __syncthreads();
-#pragma unroll 4
-  for (int q = 0; q < 16; ++q) {
-    int row, col;
-    slot_rc(q, row, col);
-    const bool ok = row < rv && col < cv && (!lower || row >= col);
-    const double a = ok ? __hip_atomic_load(src + row + (long long)col * ld, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-    sm.As[col * LP + row] = ok ? a - sm.As[col * LP + row] : 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int col = (tid >> 5) + 8 * q;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = (tid & 31) * 2 + e;
+      const bool ok = row < rv && col < cv && (!lower || row >= col);
+      sm.As[col * LP + row] = ok ? a.v[2 * q + e] - sm.As[col * LP + row] : 0.0;
+    }
   }
   __syncthreads();
 }
@@ -1300,18 +1303,23 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   PP_MARK(P, 20 + T.kind, T.i * 1000 + T.j);
   if (threadIdx.x == 0) g_stall = 0;
   PP_TRACE(P, (long long)T.idx * 4 + 1, pp_now());
+  auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
+  auto rv = [&](int r) { return min(NB, P.n - r * NB); };
+  // the task's own A tile (DP / SP: the chain's partial-sum tile; LT: A_ij), in flight from
+  // here until the epilogue
+  const int ar = T.kind == kTDP ? T.j : (T.kind == kTSP ? T.j + 1 : T.i);
+  OpTile ta;
+  if (T.kind != kTX) pp_load(ta, atile(ar, T.j), P.lda, rv(ar), T.kind == kTL ? NB : rv(T.j));
   if (!pp_accumulate(P, T, acc, abort)) return;
   PP_MARK(P, 30 + T.kind, T.i * 1000 + T.j);
   PP_TRACE(P, (long long)T.idx * 4 + 2, pp_now());
   // slot 0: workgroup | ticks polled before the K loop finished << 8
   PP_TRACE(P, (long long)T.idx * 4 + 0, blockIdx.x | (g_stall << 8));
-  auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
-  auto rv = [&](int r) { return min(NB, P.n - r * NB); };
   if (T.kind == kTDP || T.kind == kTSP) {
     // partial sums for the chain, in place in A
-    const int r = T.kind == kTDP ? T.j : T.j + 1;
+    const int r = ar;
     double* dst = atile(r, T.j);
-    pp_sub_from_a(dst, P.lda, rv(r), rv(T.j), T.kind == kTDP, acc);
+    pp_sub_tile(ta, rv(r), rv(T.j), T.kind == kTDP, acc);
     pp_store_cm(dst, P.lda, sm.As, rv(r), rv(T.j), false, T.kind == kTDP);
     pp_publish(T.kind == kTDP ? F + 2 * N * N + T.j : F + 2 * N * N + N + T.j);
     PP_TRACE(P, (long long)T.idx * 4 + 3, pp_now());
@@ -1320,7 +1328,7 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   if (T.kind == kTL) {
     // L_ij = (A_ij - acc) D_j^T
     double* dst = atile(T.i, T.j);
-    pp_sub_from_a(dst, P.lda, rv(T.i), NB, false, acc);
+    pp_sub_tile(ta, rv(T.i), NB, false, acc);
     if (!pp_wait1(F + T.j * N + T.j, abort)) return;
     int ldd;
     const double* D = pp_dptr(P, T.b, T.j, ldd);
