@@ -537,7 +537,8 @@ def main_c4(args):
     ws = kernels.PredictWorkspace()
     mean = torch.empty((bl, m), dtype=torch.float64, device=dev)
     var = torch.empty((bl, m), dtype=torch.float64, device=dev)
-    fctx = kernels.FitPredictContext(dev) if args.c4_path == "fit_predict" else None
+    fctx = kernels.FitPredictContext(dev, args.cross_start, args.aux_free_cus) \
+        if args.c4_path == "fit_predict" else None
 
     def step():
         if bl and args.c4_path == "fit_predict":

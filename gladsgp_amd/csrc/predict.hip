@@ -419,15 +419,21 @@ hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, con
   return hipGetLastError();
 }
 
-// Every chunk's TRMM into its own slab, then one finalize over all m points.
+// Every chunk's TRMM into its own slab, then one finalize over all m points.  With `ready`
+// (gp_fit_predict on a context), chunk ch's TRMM first waits for ready[ch], the event after
+// that chunk's cross-covariance on the aux stream.
 hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
                      long long strideInv, int m, const double* s_pred, double* mean,
-                     double* var, int ldo, int batch, hipStream_t stream) {
+                     double* var, int ldo, int batch, hipStream_t stream,
+                     const hipEvent_t* ready = nullptr) {
+  hipError_t e;
+  if (ready && (e = hipStreamWaitEvent(stream, ready[0], 0)) != hipSuccess) return e;
   // timing: one event pair spans the back-to-back TRMM launches (an event record between
   // launches costs a few us of stream time each); gp_profile_read reports it per launch.
   gpfit_prof_begin_n(GP_PROF_TRMM, stream, p.nchunks);
   for (int ch = 0; ch < p.nchunks; ++ch) {
-    hipError_t e = solve_chunk(p, ch, w.part + ch * p.part_elems, w.z,
+    if (ready && ch > 0 && (e = hipStreamWaitEvent(stream, ready[ch], 0)) != hipSuccess) return e;
+    e = solve_chunk(p, ch, w.part + ch * p.part_elems, w.z,
                                w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
                                s_pred, mean, var, ldo, batch, false, stream);
     if (e != hipSuccess) return e;
@@ -525,25 +531,29 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
 //   aux : the cross-covariance of every chunk (independent of the factorisation), CU-masked so
 //         that it leaves aux_free_cus CUs to the factorisation, from the factorisation's
 //         block step cross_start * n/64 on;
-//   pred: once both are done, z = L^-1 w, then per chunk the TRMM (all row tiles of the
-//         chunk, so its K* stays cached) and one mean / var pass over all m points;
+//   pred: once the factorisation is done, z = L^-1 w, then per chunk, once that chunk's
+//         cross-covariance is done, the TRMM (all row tiles of the chunk, so its K* stays
+//         cached), and one mean / var pass over all m points;
 // and joins back into `stream`.  Without a context every step runs in order on `stream`.
 struct gp_ctx_s {
   int device = -1;
   double cross_start = 0.4;
   hipStream_t fact = nullptr, aux = nullptr, pred = nullptr;
-  hipEvent_t e_start = nullptr, e_fact = nullptr, e_aux = nullptr, e_done = nullptr;
+  hipEvent_t e_start = nullptr, e_fact = nullptr, e_done = nullptr;
   hipEvent_t e_late = nullptr;   // the factorisation has turned latency-bound
+  std::vector<hipEvent_t> e_chunk;  // after chunk ch's cross-covariance (grown on demand)
 };
 
 namespace {
 
-// Defaults measured at C3 (profiles/r01): the cross-covariance on all CUs started at once
-// doubled the early, bandwidth-bound trailing updates (54 -> 123 us); on a CU-masked stream
-// that leaves 128 of 256 CUs free, a start at 40% of the block steps was best
-// (profiles/r01/ab_cross_select_exp.log, ab_update_persistent_auxmask*.log).
+// Defaults measured at C3.  Round 1 (127-launch factorisation): the cross-covariance on all
+// CUs at once doubled the early, bandwidth-bound trailing updates, so it ran CU-masked from 40%
+// of the block steps (profiles/r01/ab_cross_select_exp.log).  With the persistent
+// factorisation (1.9 ms, the cross-covariance's start event recorded before its launch) and
+// per-chunk events, leaving 32 CUs free is best: 27.03-27.11 ms/step vs 27.03-27.14 for no
+// mask, 27.31-27.57 for 64-96 and 27.79-27.88 for 128 (profiles/r02/sweep_cross_mask_r02e.log).
 constexpr double kCrossStart = 0.4;
-constexpr int kAuxFreeCUs = 128;
+constexpr int kAuxFreeCUs = 32;
 
 hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
   hipError_t e = hipGetDevice(&c->device);
@@ -566,7 +576,7 @@ hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
   } else if ((e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess) {
     return e;
   }
-  hipEvent_t* ev[5] = {&c->e_start, &c->e_fact, &c->e_aux, &c->e_done, &c->e_late};
+  hipEvent_t* ev[4] = {&c->e_start, &c->e_fact, &c->e_done, &c->e_late};
   for (hipEvent_t* p : ev)
     if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
   return hipSuccess;
@@ -584,9 +594,12 @@ hipError_t ctx_fini(gp_ctx_s* c) {
       keep(hipStreamSynchronize(x));
       keep(hipStreamDestroy(x));
     }
-  hipEvent_t ev[5] = {c->e_start, c->e_fact, c->e_aux, c->e_done, c->e_late};
+  hipEvent_t ev[4] = {c->e_start, c->e_fact, c->e_done, c->e_late};
   for (hipEvent_t x : ev)
     if (x) keep(hipEventDestroy(x));
+  for (hipEvent_t x : c->e_chunk)
+    if (x) keep(hipEventDestroy(x));
+  c->e_chunk.clear();
   if (c->device >= 0) keep(hipSetDevice(dev0));
   return first;
 }
@@ -638,12 +651,17 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   if (ws_bytes < p.bytes) return -22;
   const WS w = carve(p, ws);
   gp_ctx_s* S = static_cast<gp_ctx_s*>(ctx);
+  hipError_t e;
+#define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   if (S) {
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess || dev != S->device) return -29;
+    while ((int)S->e_chunk.size() < p.nchunks) {
+      hipEvent_t ev = nullptr;
+      GP_CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      S->e_chunk.push_back(ev);
+    }
   }
-  hipError_t e;
-#define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   hipStream_t fact = S ? S->fact : stream, aux = S ? S->aux : stream, pred = S ? S->pred : stream;
   if (S) {
     GP_CK(hipEventRecord(S->e_start, stream));
@@ -664,22 +682,26 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
     GP_CK(hipStreamWaitEvent(aux, S->e_late, 0));
   }
   // aux: cross-covariance of every chunk (one timing-event pair around all of them)
+  // (an event after each chunk: its TRMM waits for that chunk only, so the prediction starts
+  // when the factorisation ends even if later chunks' cross-covariance is still running)
   gpfit_prof_begin_n(GP_PROF_CROSS, aux, p.nchunks);
-  for (int ch = 0; ch < p.nchunks; ++ch)
+  for (int ch = 0; ch < p.nchunks; ++ch) {
     GP_CK(cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n, m, d,
                       beta, ldbeta, s, batch, aux));
+    if (S && ch + 1 < p.nchunks) GP_CK(hipEventRecord(S->e_chunk[ch], aux));
+  }
   gpfit_prof_end(GP_PROF_CROSS, aux);
   // pred: z, then TRMM + mean / var chunk by chunk.  One launch per chunk (not one for all):
   // the dispatcher interleaves another stream's kernels between launches, so a concurrent
   // factorisation is not starved behind a 25 ms grid (measured: 14 ms vs 3 ms per potrf).
   if (S) {
-    GP_CK(hipEventRecord(S->e_aux, aux));
+    GP_CK(hipEventRecord(S->e_chunk[p.nchunks - 1], aux));   // after the profile's end event
     GP_CK(hipStreamWaitEvent(pred, S->e_fact, 0));
-    GP_CK(hipStreamWaitEvent(pred, S->e_aux, 0));
   }
   GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
                           pred));
-  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, pred));
+  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, pred,
+                  S ? S->e_chunk.data() : nullptr));
   if (S) {
     GP_CK(hipEventRecord(S->e_done, pred));
     GP_CK(hipStreamWaitEvent(stream, S->e_done, 0));

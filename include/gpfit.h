@@ -178,7 +178,7 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
  *   cross_start  : fraction of the factorisation's n/64 block steps after which the
  *                  cross-covariance starts (< 0: default 0.4; 0 = at once);
  *   aux_free_cus : CUs the cross-covariance stream leaves to the factorisation (CU mask;
- *                  < 0: default 128; 0 = no mask).
+ *                  < 0: default 32; 0 = no mask).
  * gp_ctx_destroy drains the streams and frees them; call it before the HIP runtime is torn
  * down (e.g. before process exit).  A context serves one host thread at a time.
  */

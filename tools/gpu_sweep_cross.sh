@@ -7,7 +7,7 @@ TAG=${1:-sweepx}
 mkdir -p gpurun_out
 : > gpurun_out/${TAG}.log
 for rep in 1 2; do
-  for cfg in "0.4 128" "0.4 64" "0.4 192" "0.4 0" "1.0 0" "0.0 128"; do
+  for cfg in ${CFGS:-"0.4 128" "0.4 96" "0.4 64" "0.4 32" "0.4 0"}; do
     set -- $cfg
     timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu --cross-start $1 --aux-free-cus $2 > gpurun_out/${TAG}_one.log 2>&1 || { cat gpurun_out/${TAG}_one.log; exit 1; }
     python -c "
