@@ -282,6 +282,60 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
                                batch, st);
 }
 
+// z = L^-1 w for the prediction in two deterministic passes.  The one-pass trmv_kernel
+// (linalg.hip) has n/64 blocks, 64 at n = 4096, each walking up to n columns with two loads in
+// flight per lane: 90 us alone, 220 us beside the tail of the cross-covariance, and it sits
+// between the factorisation and the first TRMM (profiles/r02/step_timeline_f2d.txt).
+//   pass 1: block (rb, kt) forms row block rb's (64 rows) product with column tile kt (kZT
+//           columns; tiles on or below the diagonal only), 4 waves x 64 columns, 8 loads in
+//           flight per lane, into zp[kt][r];
+//   pass 2: z[r] = sum over kt = 0 .. last tile of r's row block of zp[kt][r], in tile order.
+// Every row r < npad is written (rows >= n are 0: L^-1 is zero-padded).  zp needs
+// batch * ceil(npad / kZT) * npad doubles; the callers lend it the TRMM's first partial-sum slab,
+// which the TRMM only writes after pass 2 (stream order).
+constexpr int kZT = 256;
+
+__global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict__ Linv, int ld,
+                                                        long long sL,
+                                                        const double* __restrict__ w, int ldw,
+                                                        double* __restrict__ zp, int npad,
+                                                        int n) {
+  const int b = blockIdx.z, rb = blockIdx.x * 64, k0 = blockIdx.y * kZT;
+  if (k0 > rb + 63 || k0 >= n) return;            // above the diagonal: pass 2 skips it
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const double* L = Linv + b * sL + rb + lane;
+  const double* wb = w + (long long)b * ldw;
+  const int kb = k0 + wv * 64;
+  const int ke = min(kb + 64, min(n, rb + 64));   // L^-1 is zero right of the diagonal
+  double acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+  for (int k = kb; k < ke; k += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (k + j < ke) acc[j] = fma(L[(long long)(k + j) * ld], wb[k + j], acc[j]);
+  }
+  __shared__ double red[4][64];
+  red[wv][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (wv == 0)
+    zp[((long long)b * gridDim.y + blockIdx.y) * npad + rb + lane] =
+        (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void trmv_sum_kernel(const double* __restrict__ zp, int nkt,
+                                                       int npad, int n, double* __restrict__ z,
+                                                       int ldz) {
+  const int b = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= npad) return;
+  const int rb = r & ~63;
+  const int last = min(rb + 63, n - 1) / kZT;     // pass 1's tiles for r's row block
+  const double* q = zp + (long long)b * nkt * npad + r;
+  double acc = 0.0;
+  for (int kt = 0; kt <= last; ++kt) acc += q[(long long)kt * npad];
+  z[(long long)b * ldz + r] = acc;
+}
+
 struct Plan {
   int npad, NI, mc, NC, nchunks, slabs;
   long long off_z, off_kt, off_part, bytes, slab_elems, part_elems;
@@ -390,6 +444,24 @@ WS carve(const Plan& p, void* ws) {
           reinterpret_cast<double*>(base + p.off_part)};
 }
 
+// z = L^-1 w into w.z (npad rows per problem): the two-pass form with the first partial-sum
+// slab as its scratch when that slab is large enough (mc >= npad / 4), else trmv_kernel.
+hipError_t trmv_pred(const Plan& p, const WS& w, const double* Linv, int ldinv,
+                     long long strideInv, const double* w_hat, int ldw, int n, int batch,
+                     hipStream_t stream) {
+  const int nkt = gp_ceil_div(p.npad, kZT);
+  if ((long long)nkt * p.npad * batch > p.part_elems)
+    return gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
+                             stream);
+  hipLaunchKernelGGL(trmv_part_kernel, dim3(p.npad / 64, nkt, batch), dim3(256), 0, stream,
+                     Linv, ldinv, strideInv, w_hat, ldw, w.part, p.npad, n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(trmv_sum_kernel, dim3(gp_ceil_div(p.npad, 256), batch), dim3(256), 0,
+                     stream, w.part, nkt, p.npad, n, w.z, p.npad);
+  return hipGetLastError();
+}
+
 hipError_t cross_chunk(const Plan& p, int ch, double* kt, const double* X, int ldx,
                        const double* Xs, int ldxs, int n, int m, int d, const double* beta,
                        int ldbeta, const double* s, int batch, hipStream_t stream) {
@@ -464,8 +536,7 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
   const WS w = carve(p, ws);
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
-  GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
-                          stream));
+  GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, stream));
   for (int ch = 0; ch < p.nchunks; ++ch) {
     gpfit_prof_begin(GP_PROF_CROSS, stream);
     GP_CK(cross_chunk(p, ch, w.kt, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch, stream));
@@ -517,8 +588,7 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
   const WS w = carve(p, ws);
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
-  GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
-                          stream));
+  GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, stream));
   GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, stream));
 #undef GP_CK
   return 0;
@@ -698,8 +768,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
     GP_CK(hipEventRecord(S->e_chunk[p.nchunks - 1], aux));   // after the profile's end event
     GP_CK(hipStreamWaitEvent(pred, S->e_fact, 0));
   }
-  GP_CK(gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
-                          pred));
+  GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, pred));
   GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, pred,
                   S ? S->e_chunk.data() : nullptr));
   if (S) {
