@@ -1560,10 +1560,19 @@ GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, int xd, F&& f) {
 
 GP_HD inline int pp_nkeys(int N, int lead, int xd) { return 4 * N - 1 + 4 * (lead + xd); }
 
+// Also zeroes the launch's flag words (dequeue head + per-tile flags) and info / logdet (in
+// place of three memset launches ahead of it: ~30 us of a C3 step).
 __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, int batch,
-                                                           int inv, int lead, int xd) {
+                                                           int inv, int lead, int xd,
+                                                           int* zero, long long nzero,
+                                                           int* info, double* logdet) {
   __shared__ int cnt[2][1024];
   const int T = threadIdx.x;
+  for (long long q = T; q < nzero; q += blockDim.x) zero[q] = 0;
+  for (int b = T; b < batch; b += blockDim.x) {
+    if (info) info[b] = 0;
+    if (logdet) logdet[b] = 0.0;
+  }
   const int nk = pp_nkeys(N, lead, xd);
   int own = 0;
   if (T < nk) pp_for_key(T, N, inv != 0, lead, xd, [&](int, int, int) { ++own; });
@@ -1678,13 +1687,14 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   const int grid = (int)(ntasks < num_cus() ? ntasks : num_cus());
   char* scr = nullptr;
   GP_CK(hipMallocAsync(reinterpret_cast<void**>(&scr), task_bytes + flag_bytes, stream));
-  GP_CK(hipMemsetAsync(scr + task_bytes, 0, flag_bytes, stream));
   int2* tasks = reinterpret_cast<int2*>(scr);
   int* head = reinterpret_cast<int*>(scr + task_bytes);
   int* flags = reinterpret_cast<int*>(scr + task_bytes + 256);
   const int lead = pp_lead(batch, grid);
+  // the schedule kernel also zeroes head + flags and info / logdet
   hipLaunchKernelGGL(pp_schedule_kernel, dim3(1), dim3(1024), 0, stream, tasks, N, batch,
-                     inv ? 1 : 0, lead, kPPXDelay);
+                     inv ? 1 : 0, lead, kPPXDelay, head, (long long)(flag_bytes / sizeof(int)),
+                     info, logdet);
   GP_CK(hipGetLastError());
   PPArgs P;
   P.A = A; P.sA = sA; P.lda = lda;
@@ -1745,12 +1755,15 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
   if (batch > 1 && strideInv < (long long)ldinv * npad) return -7;
   if (batch < 0) return -8;
   if (n == 0 || batch == 0) return 0;
-  if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
-  if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
+  const bool pp = pp_eligible(n, batch);
+  if (!pp) {   // (pp_factor's schedule kernel zeroes them)
+    if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
+    if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
+  }
   GP_CK(zero_linv(Linv, npad, ldinv, strideInv, batch, stream));
   gpfit_prof_begin(GP_PROF_POTRF, stream);
   int rc;
-  if (pp_eligible(n, batch)) {
+  if (pp) {
     // one launch, no block steps: an event asked for at a step inside the factorisation is
     // recorded before the launch (whatever waits on it runs beside the whole factorisation),
     // one asked for at k_ev >= N after it
@@ -1774,14 +1787,17 @@ extern "C" int gp_potrf(double* A, int n, int lda, long long strideA, int batch,
   if (batch > 1 && strideA < (long long)lda * n) return -4;
   if (batch < 0) return -5;
   if (n == 0 || batch == 0) return 0;
-  if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
-  if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
+  const bool pp = pp_eligible(n, batch);
+  if (!pp) {   // (pp_factor's schedule kernel zeroes them)
+    if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
+    if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
+  }
   // D_k scratch: NB x (N NB) per problem, stream-ordered (freed when the sweep has run)
   const int N = gp_ceil_div(n, NB);
   const long long sD = (long long)NB * N * NB;
   double* D = nullptr;
   GP_CK(hipMallocAsync(reinterpret_cast<void**>(&D), sizeof(double) * sD * batch, stream));
-  const int rc = pp_eligible(n, batch)
+  const int rc = pp
       ? pp_factor(A, n, lda, strideA, D, NB, sD, batch, info, logdet, false, stream)
       : potrf_sweep<kPotrf>(A, n, lda, strideA, D, NB, sD, batch, info, logdet, stream, -1,
                             nullptr);

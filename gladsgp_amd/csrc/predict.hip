@@ -263,7 +263,11 @@ hipError_t cross_kp_launch_d(const double* X, int n, int ldx, const double* Xs, 
                              int ldxs, int d, const double* beta, int ldbeta, const double* s,
                              double* Kt2, int mc, int npad, long long sK, int batch,
                              hipStream_t st) {
-  dim3 grid(gp_ceil_div(mc, 256), npad / 64, batch);
+  // only the columns the chunk's TRMM reads (its ceil(mv / BC) column tiles; zeros past mv):
+  // the 1696-point tail chunk of C3 no longer computes all 16384 columns (14.7% of a step's
+  // cross-covariance work)
+  const int cols = min(mc, gp_ceil_div(mv, BC) * BC);
+  dim3 grid(gp_ceil_div(cols, 256), npad / 64, batch);
   hipLaunchKernelGGL((cross_kp_kernel<D>), grid, dim3(256), 0, st, X, n, ldx, Xs, mv, ldxs, d,
                      beta, ldbeta, s, Kt2, mc, sK);
   return hipGetLastError();
