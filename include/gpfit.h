@@ -174,7 +174,8 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
 
 /*
  * Execution context of gp_fit_predict, created and destroyed by the caller on the current
- * device: three streams (factorisation | cross-covariance | prediction) and their events.
+ * device: three streams (factorisation | cross-covariance | prediction) and their events (one
+ * per test-point chunk after its cross-covariance, created on the first call that needs them).
  *   cross_start  : fraction of the factorisation's n/64 block steps after which the
  *                  cross-covariance starts (< 0: default 0.4; 0 = at once);
  *   aux_free_cus : CUs the cross-covariance stream leaves to the factorisation (CU mask;
@@ -191,8 +192,9 @@ int gp_ctx_destroy(void* ctx);
  *   mean / var at the m test points (as gp_predict).
  * With ctx == NULL every step runs in order on `stream`.  With a context it forks from
  * `stream` into the context's streams (Gram + factorisation | cross-covariance of every chunk,
- * CU-masked, from the factorisation's latency-bound phase on | then per chunk the TRMM and one
- * mean/var pass) and joins back: the caller sees one stream-ordered operation.  `ws` holds
+ * CU-masked, beside the factorisation | once the factorisation is done z = L^-1 w, then per
+ * chunk, once that chunk's cross-covariance is done, its TRMM, and one mean/var pass) and joins
+ * back: the caller sees one stream-ordered operation.  `ws` holds
  * gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes.  The prediction runs whatever info
  * says: mean / var of a problem with info[b] != 0 are unspecified (check info).
  * Replaces the reference's fit-then-predict sequence per GP (SEPIA likelihood factorisation +
