@@ -291,13 +291,13 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
 // flight per lane: 90 us alone, 220 us beside the tail of the cross-covariance, and it sits
 // between the factorisation and the first TRMM (profiles/r02/step_timeline_f2d.txt).
 //   pass 1: block (rb, kt) forms row block rb's (64 rows) product with column tile kt (kZT
-//           columns; tiles on or below the diagonal only), 4 waves x 64 columns, 8 loads in
-//           flight per lane, into zp[kt][r];
+//           = 128 columns; tiles on or below the diagonal only: ~1056 blocks at n = 4096),
+//           4 waves x 32 columns, 8 loads in flight per lane, into zp[kt][r];
 //   pass 2: z[r] = sum over kt = 0 .. last tile of r's row block of zp[kt][r], in tile order.
-// Every row r < npad is written (rows >= n are 0: L^-1 is zero-padded).  zp needs
-// batch * ceil(npad / kZT) * npad doubles; the callers lend it the TRMM's first partial-sum slab,
-// which the TRMM only writes after pass 2 (stream order).
-constexpr int kZT = 256;
+// Every row r < npad is written (rows >= n are 0: L^-1 is zero-padded).  zp (batch *
+// ceil(npad / kZT) * npad doubles, 1 MB per problem at n = 4096) is its own workspace region.
+constexpr int kZT = 128;
+constexpr int kZW = kZT / 4;   // columns per wave
 
 __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict__ Linv, int ld,
                                                         long long sL,
@@ -309,8 +309,8 @@ __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const double* L = Linv + b * sL + rb + lane;
   const double* wb = w + (long long)b * ldw;
-  const int kb = k0 + wv * 64;
-  const int ke = min(kb + 64, min(n, rb + 64));   // L^-1 is zero right of the diagonal
+  const int kb = k0 + wv * kZW;
+  const int ke = min(kb + kZW, min(n, rb + 64));  // L^-1 is zero right of the diagonal
   double acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.0;
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void trmv_sum_kernel(const double* __restrict_
 
 struct Plan {
   int npad, NI, mc, NC, nchunks, slabs;
-  long long off_z, off_kt, off_part, bytes, slab_elems, part_elems;
+  long long off_z, off_zp, off_kt, off_part, bytes, slab_elems, part_elems;
 };
 
 // slabs = 1: one cross-covariance chunk and one partial-sum slab at a time (gp_predict, which
@@ -377,11 +377,13 @@ Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
   p.slabs = all_slabs ? p.nchunks : 1;
   p.slab_elems = (long long)batch * mc * p.npad;
   long long z = (long long)batch * p.npad;
+  long long zp = (long long)batch * gp_ceil_div(p.npad, kZT) * p.npad;   // trmv partials
   long long kt = p.slab_elems * p.slabs;
   p.part_elems = (long long)batch * 2 * p.NI * mc;
   const long long part = p.part_elems * p.slabs;
   p.off_z = 0;
-  p.off_kt = ((z * 8 + 255) / 256) * 256;
+  p.off_zp = ((z * 8 + 255) / 256) * 256;
+  p.off_kt = p.off_zp + ((zp * 8 + 255) / 256) * 256;
   p.off_part = p.off_kt + ((kt * 8 + 255) / 256) * 256;
   p.bytes = p.off_part + part * 8;
   return p;
@@ -439,30 +441,27 @@ int check_solve(const double* Linv, int ldinv, long long strideInv, int n, const
 }
 
 struct WS {
-  double *z, *kt, *part;
+  double *z, *zp, *kt, *part;
 };
 
 WS carve(const Plan& p, void* ws) {
   char* base = static_cast<char*>(ws);
-  return {reinterpret_cast<double*>(base + p.off_z), reinterpret_cast<double*>(base + p.off_kt),
-          reinterpret_cast<double*>(base + p.off_part)};
+  return {reinterpret_cast<double*>(base + p.off_z), reinterpret_cast<double*>(base + p.off_zp),
+          reinterpret_cast<double*>(base + p.off_kt), reinterpret_cast<double*>(base + p.off_part)};
 }
 
-// z = L^-1 w into w.z (npad rows per problem): the two-pass form with the first partial-sum
-// slab as its scratch when that slab is large enough (mc >= npad / 4), else trmv_kernel.
+// z = L^-1 w into w.z (npad rows per problem), two passes through w.zp (the same arithmetic
+// whatever the chunking, so results stay bit-identical across m_chunk).
 hipError_t trmv_pred(const Plan& p, const WS& w, const double* Linv, int ldinv,
                      long long strideInv, const double* w_hat, int ldw, int n, int batch,
                      hipStream_t stream) {
   const int nkt = gp_ceil_div(p.npad, kZT);
-  if ((long long)nkt * p.npad * batch > p.part_elems)
-    return gpfit_trmv_launch(Linv, ldinv, strideInv, w_hat, ldw, w.z, p.npad, p.npad, n, batch,
-                             stream);
   hipLaunchKernelGGL(trmv_part_kernel, dim3(p.npad / 64, nkt, batch), dim3(256), 0, stream,
-                     Linv, ldinv, strideInv, w_hat, ldw, w.part, p.npad, n);
+                     Linv, ldinv, strideInv, w_hat, ldw, w.zp, p.npad, n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(trmv_sum_kernel, dim3(gp_ceil_div(p.npad, 256), batch), dim3(256), 0,
-                     stream, w.part, nkt, p.npad, n, w.z, p.npad);
+                     stream, w.zp, nkt, p.npad, n, w.z, p.npad);
   return hipGetLastError();
 }
 

@@ -200,9 +200,8 @@ def test_predict_c2_full_m10k(dev, golden_dir):
 @pytest.mark.parametrize("n,m,d,chunk", [(1, 1, 1, 0), (5, 51, 1, 0), (65, 129, 3, 0),
                                          (130, 300, 8, 128), (256, 1000, 8, 384),
                                          (700, 257, 16, 0),
-                                         # z = L^-1 w: two-pass form with npad = 1152 (an odd
-                                         # number of 128-row tiles), and the one-pass fallback
-                                         # (chunk < npad / 4: the slab cannot hold the partials)
+                                         # z = L^-1 w's two passes at npad = 1152 (an odd
+                                         # number of 128-row tiles), default and small chunks
                                          (1100, 2000, 8, 0), (1100, 300, 8, 128)])
 def test_predict_edges(dev, n, m, d, chunk):
     rng = np.random.default_rng(n * 7 + m)
