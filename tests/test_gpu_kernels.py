@@ -287,8 +287,13 @@ def test_two_phase_predict_and_overlap_match_single(dev):
     with kernels.FitPredictContext(dev) as fctx:
         m3, v3, ch3 = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
                                           _t(s, dev), _t(W, dev), m_chunk=1024, ctx=fctx)
+        # the same context again with more chunks (its per-chunk events grow on demand; each
+        # chunk's TRMM waits for its own chunk's cross-covariance only)
+        m5, v5, _ = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
+                                        _t(s, dev), _t(W, dev), m_chunk=384, ctx=fctx)
         torch.cuda.synchronize()
     assert torch.equal(m1, m3) and torch.equal(v1, v3)
+    assert torch.equal(m1, m5) and torch.equal(v1, v5)
     assert torch.equal(ch3.L, ch.L) and torch.equal(ch3.Linv, ch.Linv)
     assert torch.equal(ch3.logdet, ch.logdet) and int(ch3.info.abs().sum()) == 0
     m4, v4, _ = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
