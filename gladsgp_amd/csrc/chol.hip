@@ -1525,7 +1525,9 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
 // more workgroups than problems drains.  pp_lead() takes W = kPPLead only while every problem's
 // blocked early tasks plus its chain fit in the grid with a worker to spare (batch 32 at
 // n = 1024 on 256 workgroups deadlocked with W = 6 for every problem: 32 x 24 > 224).
-constexpr int kPPLead = 6;
+// W = 4: n = 4096 1.855-1.857 ms median vs 1.880-1.890 at W = 6 and 1.896-1.909 at 8, batch 32
+// unchanged (profiles/r02/ab_pp_lead_xd.log, XT delay 6 / 8 / 11 equal within noise).
+constexpr int kPPLead = 4;
 constexpr int kPPLeadBlocked = 4 * kPPLead + 2;   // per-problem bound on blocked early tasks
 constexpr int kPPBand = 3;
 constexpr int kPPXDelay = 8;   // XT tasks: 8 chain steps after the late LT tasks of their row
