@@ -156,133 +156,46 @@ def read_prof(pid):
     return cnt.value, max(tot.value, 1e-9)   # events off (GPFIT_BENCH_NOEVENTS=1): no data
 
 
-def split_rank0(m: int, N: int, t_fact: float, t_point: float) -> int:
-    """Test points for rank 0 in the pipelined schedule (it also factorises the next GP): the
-    factorisation in test-point equivalents e = t_fact / t_point is added to rank 0's share,
-    so every rank's step is (m + e) / N points' worth.  (A partial residency wave of the TRMM
-    costs about its share: blocks alone on a CU run about twice as fast, measured with the
-    1696-point tail launch of C3 at 0.53 ms against 1.03 ms for a full wave.)"""
-    m1 = int(np.ceil((m + t_fact / t_point) / N))
-    return max(0, m - (N - 1) * m1)
-
-
 def c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed):
-    """N > 1: a two-stage pipeline over a stream of GPs ("rank 0 factorises and
-    broadcasts L").  GP k has hyperparameters beta (1 + 1e-3 (k mod 2)), so consecutive steps
-    are different GPs.  In step k rank 0 builds GP k+1's Gram and L, L^-1 (the persistent
-    factorisation) and broadcasts L^-1 over RCCL (async, its lower triangle packed, into the other buffer of a
-    double-buffered pair), while every rank predicts GP k on its block of the 100k test points
-    and the (mean, var) blocks are gathered to rank 0.  Rank 0's block is shortened by the
-    factorisation's time in test-point equivalents (measured here: t_fact / t_point), so the
-    ranks finish together.  Every step still does one full Gram + factorisation and one full
-    100k-point prediction; a GP's latency is two steps.
+    """N > 1 headline: gladsgp_amd.sharded.PipelinedPredictor over a stream of GPs (SURVEY §8e:
+    "rank 0 factorises and broadcasts L").  GP k has hyperparameters beta (1 + 1e-3 (k mod 2)),
+    so consecutive steps are different GPs.  In step k rank 0 builds GP k+1's Gram and L, L^-1
+    (the persistent factorisation) and broadcasts L^-1 over RCCL (async, its lower triangle
+    packed, double-buffered), while every rank predicts GP k on its block of the 100k test
+    points and the (mean, var) blocks are gathered to rank 0.  Rank 0's block is shortened by
+    the factorisation's time in test-point equivalents (measured by the package's calibrate),
+    so the ranks finish together.  Every step still does one full Gram + factorisation and one
+    full 100k-point prediction; a GP's latency is two steps.
     Returns the timing, the split and a check of the last step against a direct single-rank
     computation of the same GP on rank 0."""
-    import torch.distributed as dist
+    from gladsgp_amd.sharded import PipelinedPredictor
     dev = ctx.device
-    N, rank = ctx.world, ctx.rank
     n, d = X.shape
     m = Xs.shape[0]
-    npad = kernels.padded_n(n)
     Xd = torch.as_tensor(X, device=dev)
     yd = torch.as_tensor(y, device=dev).reshape(1, n)
     sd = torch.tensor([s], dtype=torch.float64, device=dev)
     dd = torch.tensor([delta], dtype=torch.float64, device=dev)
     betas = [torch.as_tensor(beta * (1.0 + 1e-3 * j), device=dev).reshape(1, d) for j in (0, 1)]
-    linv = [torch.zeros((1, npad, npad), dtype=torch.float64, device=dev) for _ in range(2)]
-    info = torch.zeros(1, dtype=torch.int32, device=dev)
-    logdet = torch.zeros(1, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-
-    def factor(k):                      # rank 0: GP k's Gram -> L, L^-1 into linv[k % 2]
-        G = kernels.gram(Xd, betas[k % 2], sd, dd)
-        _capi.call("gp_potrf_inv", G.data_ptr(), n, n, n * n, linv[k % 2].data_ptr(), npad,
-                   npad * npad, 1, info.data_ptr(), logdet.data_ptr(), stream)
-
-    # calibration on rank 0: factorisation time and per-point prediction time
-    calib = torch.zeros(2, dtype=torch.float64, device=dev)
-    if rank == 0:
-        mc = min(m, 16384)
-        Xc = torch.as_tensor(Xs[:mc], device=dev).contiguous()
-        ch = kernels.Cholesky(n, None, linv[0], info, logdet)
-        tf, tp = [], []
-        for _ in range(3):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            factor(0)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            kernels.predict(ch, Xd, Xc, betas[0], sd, sd, yd)
-            torch.cuda.synchronize()
-            tf.append(t1 - t0)
-            tp.append((time.perf_counter() - t1) / mc)
-        calib[0], calib[1] = sorted(tf)[1], sorted(tp)[1]
-        del Xc
-    gdist.broadcast_(ctx, calib)
-    t_fact, t_point = float(calib[0]), float(calib[1])
-    m0 = split_rank0(m, N, t_fact, t_point)
-    rest = [gdist.shard_range(m - m0, r, N - 1) for r in range(N - 1)]
-    counts = [m0] + [b - a for a, b in rest]
-    lo = 0 if rank == 0 else m0 + rest[rank - 1][0]
-    ml = counts[rank]
-    Xsd = torch.as_tensor(Xs[lo:lo + ml], device=dev).contiguous()
-    out = torch.empty((2, max(ml, 1)), dtype=torch.float64, device=dev)
-    ws = kernels.PredictWorkspace()
-    chs = [kernels.Cholesky(n, None, linv[j], info, logdet) for j in (0, 1)]
-    state = {"k": 0, "pending": None, "res": None}
-
-    # L^-1 travels packed: its nonzero part, column c (col-major) from row c on, half the bytes
-    # of the padded square.  Rank 0 gathers it after the factorisation; the others scatter it
-    # into receive buffers that were zero-filled once (the upper triangle never changes).
-    tri = torch.triu_indices(npad, npad, device=dev)     # (c, r), r >= c, of the [c][r] view
-    flat = tri[0] * npad + tri[1]
-    del tri
-    packed = [torch.empty(flat.numel(), dtype=torch.float64, device=dev) for _ in range(2)]
-
-    if ctx.backend == "nccl":
-        def bcast(k):                   # async on RCCL's stream, overlapping the prediction
-            if rank == 0:
-                torch.index_select(linv[k % 2].view(-1), 0, flat, out=packed[k % 2])
-            return dist.broadcast(packed[k % 2], src=0, async_op=True)
-    else:
-        def bcast(k):                   # gloo (the 1-GPU tests): host-staged and synchronous
-            if rank == 0:
-                torch.index_select(linv[k % 2].view(-1), 0, flat, out=packed[k % 2])
-            gdist.broadcast_(ctx, packed[k % 2])
-            return None
-
-    # prologue: GP 0 factorised and broadcast
-    if rank == 0:
-        factor(0)
-    state["pending"] = bcast(0)
+    gps = [(betas[j], sd, dd, sd) for j in (0, 1)]
+    pp = PipelinedPredictor(ctx, Xd, torch.as_tensor(Xs, device=dev), yd, calib_gp=gps[0],
+                            m_chunk=args.m_chunk)
+    pp.start(gps[0])
+    state = {"res": None}
 
     def pipe_step():
-        k = state["k"]
-        if rank == 0:
-            factor(k + 1)
-        nxt = bcast(k + 1)
-        if state["pending"] is not None:
-            state["pending"].wait()
-        if rank != 0:                   # GP k's L^-1 from its packed broadcast
-            linv[k % 2].view(-1).index_copy_(0, flat, packed[k % 2])
-        if ml:
-            kernels.predict(chs[k % 2], Xd, Xsd, betas[k % 2], sd, sd, yd, m_chunk=args.m_chunk,
-                            workspace=ws, out=(out[0:1, :ml], out[1:2, :ml]))
-        state["res"] = gdist.gather_cols(ctx, out[:, :ml], counts)
-        state["pending"] = nxt
-        state["k"] = k + 1
+        state["res"] = pp.step(gps[(pp.k + 1) % 2])
 
     for _ in range(args.warmup):
         pipe_step()
     torch.cuda.synchronize()
     elapsed = timed(pipe_step, args.steps)
-    if state["pending"] is not None:
-        state["pending"].wait()
+    pp.finish()
     torch.cuda.synchronize()
     check = None
-    if rank == 0:
-        # the last step predicted GP k_last = state["k"] - 1: recompute it directly on a sample
-        k_last = state["k"] - 1
+    if ctx.rank == 0:
+        # the last step predicted GP k_last = pp.k - 1: recompute it directly on a sample
+        k_last = pp.k - 1
         ns = min(2000, m)
         G = kernels.gram(Xd, betas[k_last % 2], sd, dd)
         ch = kernels.cholesky_inverse(G)
@@ -295,8 +208,50 @@ def c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed):
         check = {"gp": k_last, "points": ns, "max_abs_dmean": dm, "max_abs_dvar": dv}
         if not (dm <= 1e-10 * max(1.0, float(mu.abs().max())) and dv <= 1e-12):
             raise RuntimeError(f"pipelined result differs from the direct computation: {check}")
-    return {"elapsed": elapsed, "counts": counts, "t_fact_ms": t_fact * 1e3,
-            "t_point_us": t_point * 1e6, "check": check}
+    return {"elapsed": elapsed, "counts": pp.counts, "t_fact_ms": pp.t_fact * 1e3,
+            "t_point_us": pp.t_point * 1e6, "check": check}
+
+
+def _free_port() -> int:
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(args) -> int | None:
+    """``--gpus N`` (N > 1) run without a torch.distributed launcher (no WORLD_SIZE): start the N
+    ranks as ``torch.distributed.run`` in a child process of this parent, which has touched no
+    GPU (nothing here initialises HIP), and return the child's exit code.  Under a launcher (or
+    N = 1) return None and run in-process."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this host
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def main_dry_run(args):
+    """``--dry-run``: the launch / rendezvous / max-over-ranks / JSON path with no GPU work (gloo
+    on the host) -- what the CPU test of ``--gpus N`` exercises."""
+    ctx = gdist.init_from_env("cpu", backend="gloo")
+    if ctx.world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but {ctx.world} ranks joined")
+    gdist.barrier(ctx)
+    t0 = time.perf_counter()
+    gdist.barrier(ctx)
+    elapsed = gdist.max_over_ranks(ctx, time.perf_counter() - t0)
+    if ctx.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "predictions/s",
+                          "n_gpus": ctx.world, "steps": 0, "warmup": 0,
+                          "ms_per_step": elapsed * 1e3, "higher_is_better": True,
+                          "dry_run": True}), flush=True)
 
 
 def main():
@@ -316,7 +271,11 @@ def main():
                     help="testing only: every rank on cuda:0 over gloo (host-staged collectives)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: headline = the redundant-factorisation strong split only")
-    ap.add_argument("--workload", choices=("c3", "c4", "fit"), default="c3")
+    ap.add_argument("--workload", choices=("c3", "c4", "fit", "latency"), default="c3")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch / rendezvous / JSON path only, no GPU work (gloo on the host)")
+    ap.add_argument("--latency-points", type=int, default=20,
+                    help="latency: test points timed one at a time (time_predictions.py:68)")
     ap.add_argument("--ny", type=int, default=1347945, help="fit: field size per run")
     ap.add_argument("--fit-pcs", type=int, default=8, help="fit: principal components")
     ap.add_argument("--serial", action="store_true",
@@ -332,13 +291,23 @@ def main():
                          "step (measured 1-3%% slower at C4: its cross-covariance, 5x the "
                          "batched potrf, stretches the potrf and the TRMM waits for all of it)")
     args = ap.parse_args()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.dry_run:
+        return main_dry_run(args)
     if args.workload == "c4":
         return main_c4(args)
     if args.workload == "fit":
         return main_fit(args)
+    if args.workload == "latency":
+        return main_latency(args)
 
     ctx = (gdist.init_from_env("cuda", backend="gloo", device_index=0) if args.share_gpu
            else gdist.init_from_env("cuda"))
+    if ctx.world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but {ctx.world} ranks joined "
+                         "(WORLD_SIZE); refusing to report a mislabelled number")
     dev = ctx.device
     n, m, d = args.n, args.m, args.d
     X, y, beta, Xs, s, delta = c3_inputs(n, m, d)
@@ -371,17 +340,21 @@ def main():
         gdist.barrier(ctx)
         return gdist.max_over_ranks(ctx, time.perf_counter() - t0)
 
+    from gladsgp_amd import sharded
+    Xs_all = torch.as_tensor(Xs, device=dev)
     gathered = [None]
 
-    def strong_step():
-        ch = step()
-        gathered[0] = gdist.gather_cols(ctx, out, counts)   # (2, m) on rank 0
-        return ch
+    def strong_step(check=False):
+        # package API (SURVEY §8e single-output GP): rank r predicts its block of the m points
+        # with gp_fit_predict (redundant factorisation) and the blocks are gathered to rank 0
+        gathered[0] = sharded.predict_sharded(ctx, Xd, Xs_all, bd, sd, dd, sd, yd,
+                                              mode="redundant", counts=counts,
+                                              m_chunk=args.m_chunk, fctx=fctx, workspace=ws,
+                                              check=check)
 
-    for _ in range(args.warmup):
-        ch = strong_step()
+    for i in range(args.warmup):
+        strong_step(check=(i == 0))      # the first warmup step checks info (syncs)
     torch.cuda.synchronize()
-    ch.check()
     if os.environ.get("GPFIT_BENCH_NOEVENTS") != "1":
         _capi.call("gp_profile_enable", 64 * (args.steps + 1))
     _capi.call("gp_profile_reset")
@@ -407,7 +380,7 @@ def main():
                         "no collective)"}
         del Xwd, ow
 
-    res = gathered[0]
+    res = None if gathered[0] is None else torch.stack(gathered[0])   # (2, m) on rank 0
     if fctx is not None:
         fctx.close()
     pipe = None
@@ -599,6 +572,150 @@ def main_c4(args):
     }
     assert out is not None and out[0].shape == (P, m)
     print(json.dumps(line), flush=True)
+
+
+def synthetic_field(n: int, d: int, ny: int, seed: int = 0):
+    """A smooth low-rank float32 ensemble of the reference's shape (n runs x ny nodes; the
+    reference stores Y_physical as (ny, n), time_predictions.py:39): 12 space modes with
+    decaying weight, seeded, plus 1e-3 noise."""
+    rng = np.random.default_rng(seed)
+    t = rng.random((n, d))
+    nm = 12
+    modes = (rng.standard_normal((nm, ny)) * (0.6 ** np.arange(nm))[:, None]).astype(np.float32)
+    coef = np.stack([np.sin(2 * np.pi * t @ rng.uniform(0, 1, d) + k) for k in range(nm)], 1)
+    Y = coef.astype(np.float32) @ modes
+    Y += 1e-3 * rng.standard_normal(Y.shape, dtype=np.float32)
+    return t, Y
+
+
+def synthetic_samples(d: int, P: int, N: int = 512, seed: int = 5) -> dict:
+    """A posterior-sample dict in SEPIA's layout (betaU (N, (d+1) P), lamUz/lamWs (N, P), lamWOs
+    (N, 1)) drawn around GPMSA-typical values (prediction timing needs samples, not a fit)."""
+    rng = np.random.default_rng(seed)
+    return {"betaU": rng.uniform(0.2, 3.0, (N, (d + 1) * P)),
+            "lamUz": rng.uniform(0.5, 3.0, (N, P)),
+            "lamWs": rng.uniform(200, 3000, (N, P)),
+            "lamWOs": rng.uniform(50, 500, (N, 1))}
+
+
+def main_latency(args):
+    """The reference's own prediction-timing harness, time_predictions.py:53,68-101, at its
+    configuration: m = 256 training runs (train_config.py:9), p = 8 PCs (train_config.py:75),
+    32 posterior samples (``get_samples(numsamples=32, nburn=256)``, cast to float32), one test
+    point per call, a 1,347,945-node field.  Per test point, timed exactly as the harness does:
+        preds = SepiaEmulatorPrediction(samples=, model=, t_pred=xi)   (here EmulatorPrediction)
+        preds.w = preds.w.astype(float32); emulator_preds = preds.get_y()      -> emulator
+        error_preds[j] = sd_y * N(0, 1/sqrt(lamWOs_j)) (host numpy); y = emulator + error
+                                                                                 -> full
+    plus the device-side alternative get_y(add_error=True) beside it.  Seconds per prediction
+    (lower is better); the CPU baseline runs the oracle's restatement of the same per-point
+    work (S x P GP solves at n = 256 + the float32 field reconstruction) on the host."""
+    import shutil
+    import tempfile
+    from gladsgp_amd import model as gmodel
+    from gladsgp_amd.emulator import EmulatorPrediction
+    dev = torch.device("cuda", 0)
+    n, d, P, S, ny = 256, 8, 8, 32, args.ny
+    t, Y = synthetic_field(n, d, ny)
+    tmp = tempfile.mkdtemp(prefix="gladsgp_lat_")
+    try:
+        np.random.seed(0)
+        data, model = gmodel.init_model(t.astype(np.float32), Y, "lat", P, data_dir=tmp,
+                                        device=dev, verbose=False)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    model.set_samples(synthetic_samples(d, P))
+    samples = model.get_samples(numsamples=32, nburn=256)           # time_predictions.py:53
+    for key in samples.keys():
+        samples[key] = samples[key].astype(np.float32)
+    sd_y = data.sim_data.y_sd.cpu().numpy().astype(np.float32)   # time_predictions.py:65-66
+    t_test = np.random.default_rng(9).random((args.latency_points + args.warmup, d)).astype(
+        np.float32)
+    dt_em, dt_err, dt_y, dt_dev = [], [], [], []
+    for i in range(t_test.shape[0]):
+        xi = t_test[i:i + 1]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        preds = EmulatorPrediction(samples=samples, model=model, t_pred=xi)
+        preds.w = preds.w.astype(np.float32)
+        emulator_preds = preds.get_y()
+        t1 = time.perf_counter()
+        error_preds = np.zeros(emulator_preds.shape, dtype=np.float32)
+        for j in range(error_preds.shape[0]):
+            error_preds[j] = sd_y * np.random.normal(
+                scale=1 / np.sqrt(samples["lamWOs"][j])).astype(np.float32)
+        y_preds = emulator_preds + error_preds
+        t2 = time.perf_counter()
+        # the device-side error term (one scalar per sample, time_predictions.py:84-87 form)
+        t3 = time.perf_counter()
+        preds2 = EmulatorPrediction(samples=samples, model=model, t_pred=xi)
+        preds2.w = preds2.w.astype(np.float32)
+        y_dev = preds2.get_y(add_error=True, per_point=False)
+        t4 = time.perf_counter()
+        if i >= args.warmup:
+            dt_em.append(t1 - t0)
+            dt_err.append(t2 - t1)
+            dt_y.append(t2 - t0)
+            dt_dev.append(t4 - t3)
+    assert y_preds.shape == (S, 1, ny) and y_dev.shape == (S, 1, ny)
+    assert y_preds.dtype == np.float32 and np.all(np.isfinite(y_preds))
+    value = float(np.mean(dt_y))
+    out_mb = S * ny * 4 / 1e6
+    line = {
+        "metric": "GladsGP prediction latency (time_predictions.py harness): seconds per "
+                  "prediction, n=256 p=8 S=32 ny=1,347,945, one test point per call",
+        "value": value, "unit": "s", "n_gpus": 1, "steps": len(dt_y), "warmup": args.warmup,
+        "ms_per_step": value * 1e3, "higher_is_better": False, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64 (GP), f32 (field, as the reference casts)",
+        "data": "synthetic low-rank float32 field of the reference's shape, synthetic "
+                "posterior samples (GPMSA-typical ranges), seeded",
+        "config": {"workload": "time_predictions.py: EmulatorPrediction -> .w float32 cast -> "
+                               "get_y() -> host error term", "n_train": n, "pcs": P,
+                   "samples": S, "ny": ny, "points": len(dt_y)},
+        "breakdown": {"emulator_s": float(np.mean(dt_em)), "error_s": float(np.mean(dt_err)),
+                      "full_s": value, "full_device_error_s": float(np.mean(dt_dev)),
+                      "field_MB_per_prediction": out_mb,
+                      "note": "emulator = SEPIA-equivalent prediction + get_y (incl. the "
+                              "device-to-host copy of the float32 field, as the reference "
+                              "returns numpy); error = the harness's own host numpy loop"},
+        "roofline": None, "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        line["cpu_baseline"] = cpu_latency_baseline(data, model, samples, t_test[0:1], sd_y)
+    print(json.dumps(line), flush=True)
+
+
+def cpu_latency_baseline(data, model, samples, xi, sd_y, reps: int = 3):
+    """The oracle's restatement of one time_predictions.py iteration on the host: the S x P
+    GP solves at n = 256 (Gram, Cholesky, mean / variance at one point: gp_ref.sepia_predict_w)
+    + the float32 field reconstruction y = (w K) sd + mu and the harness's error term.  Median
+    of ``reps``; the reference re-factorises per call exactly like this."""
+    from oracle import gp_ref
+    t = data.sim_data.t_dev.cpu().numpy()
+    w_hat = model.w_hat.cpu().numpy()
+    lam = model.LamSim.cpu().numpy()
+    K = data.sim_data.K.cpu().numpy().astype(np.float32)
+    mu = data.sim_data.y_mean.cpu().numpy().astype(np.float32)
+    sd = data.sim_data.y_sd.cpu().numpy().astype(np.float32)
+    runs = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        w, _ = gp_ref.sepia_predict_w(t, xi.astype(np.float64), w_hat, samples, lam)
+        w = w.astype(np.float32)
+        y = (np.einsum("smp,py->smy", w, K) * sd + mu).astype(np.float32)
+        e = np.zeros(y.shape, dtype=np.float32)
+        for j in range(y.shape[0]):
+            e[j] = sd_y * np.random.normal(scale=1 / np.sqrt(samples["lamWOs"][j])).astype(
+                np.float32)
+        _ = y + e
+        runs.append(time.perf_counter() - t0)
+    runs.sort()
+    v = runs[len(runs) // 2]
+    return {"value": v, "unit": "s", "cores": _CPU_THREADS, "kind": "port",
+            "sample": (f"oracle/gp_ref numpy (fp64 GP solves, float32 field), OpenBLAS "
+                       f"{_CPU_THREADS} threads on {cpu_model()}: one time_predictions.py "
+                       f"iteration (S x P = {w_hat.shape[1] * len(samples['lamUz'])} GPs at "
+                       f"n = {t.shape[0]}, field of {K.shape[1]} nodes), median of {reps}")}
 
 
 # reference fit timings (BASELINE.md; timing.csv:9, n=512 P=8: PCA incl. load/standardise,

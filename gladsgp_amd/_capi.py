@@ -20,6 +20,7 @@ from ._build import LIB_PATH
 c_int, c_ll, c_void_p, c_double_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p
 
 GPFIT_ERR_HIP = -1000
+GPFIT_ERR_INTERNAL = -2000
 GPFIT_ERR_RCCL = -3000
 
 # name -> (restype, argtypes); pointers are passed as integers (tensor.data_ptr()).
@@ -34,6 +35,12 @@ SIGNATURES = {
     "gp_potrf_inv": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_ll, c_int,
                              c_void_p, c_void_p, c_void_p]),
     "gp_potrf": (c_int, [c_void_p, c_int, c_int, c_ll, c_int, c_void_p, c_void_p, c_void_p]),
+    "gp_potrf_inv_ws_bytes": (c_ll, [c_int, c_int]),
+    "gp_potrf_inv_ws": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_ll, c_int,
+                                c_void_p, c_void_p, c_void_p, c_ll, c_void_p]),
+    "gp_potrf_ws_bytes": (c_ll, [c_int, c_int]),
+    "gp_potrf_ws": (c_int, [c_void_p, c_int, c_int, c_ll, c_int, c_void_p, c_void_p, c_void_p,
+                            c_ll, c_void_p]),
     "gp_trtri": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_ll, c_int, c_void_p,
                          c_void_p]),
     "gp_predict_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
@@ -67,6 +74,7 @@ SIGNATURES = {
     "gp_loglik": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                           c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,
                           c_void_p]),
+    "gp_loglik_status": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "gp_realize": (c_int, [c_void_p, c_void_p, c_ll, ctypes.c_ulonglong, ctypes.c_ulonglong,
                            c_void_p, c_void_p]),
     "gp_dgemm_ws_bytes": (c_ll, [c_int, c_int, c_int]),
@@ -91,6 +99,7 @@ SIGNATURES = {
     "gp_profile_enable": (c_int, [c_int]),
     "gp_profile_reset": (c_int, []),
     "gp_profile_read": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
+    "gp_set_poll_budget": (c_ll, [c_ll]),
 }
 
 PROF_GRAM, PROF_POTRF, PROF_TRMM, PROF_CROSS = 0, 1, 2, 3
@@ -106,6 +115,9 @@ class GPFitError(RuntimeError):
     def __init__(self, func: str, rc: int):
         if rc <= GPFIT_ERR_RCCL:
             msg = f"{func}: RCCL error {GPFIT_ERR_RCCL - rc} (or librccl not loadable)"
+        elif rc == GPFIT_ERR_INTERNAL:
+            msg = (f"{func}: internal error: a factorisation gave up (info = -1, a bounded wait "
+                   "of the persistent kernel ran out) -- results since the last check are invalid")
         elif rc <= GPFIT_ERR_HIP:
             msg = f"{func}: HIP error {GPFIT_ERR_HIP - rc}"
         else:

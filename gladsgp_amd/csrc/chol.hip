@@ -27,6 +27,7 @@
 //                             X_kc panels and R tiles (LAPACK dtrtri('L','N') + padding).
 #include "gpfit_common.h"
 #include <cstdlib>
+#include <vector>
 #include "gpfit_profile.h"
 #include "gpfit_internal.h"
 #include "../../include/gpfit.h"
@@ -909,36 +910,55 @@ __global__ void trtri_info_kernel(int* __restrict__ info, int batch) {
 // chain needs next at the front.
 // Hand-offs follow MI355X_MICROARCH.md's acquire-free form: produced tiles are stored with
 // sc1 (write-through) 16-B stores, each storing wave waits vmcnt(0), the workgroup barriers,
-// one lane stores the flag (sc1); consumers poll flags with sc1 loads and read every produced
-// byte with sc1 loads.  Every wait also watches the problem's abort word (non-PD pivot) and a
-// poll budget, so no path can spin forever.
+// one lane stores the flag (sc1); consumers poll flags with sc1 loads.  Tiles that pass
+// through in-place partial sums (near-diagonal L tiles) are read with sc1 loads; every other
+// produced tile is written once and read only after its flag, with plain (L2-cached) loads --
+// but only when no 128-B cache line straddles two tiles (PPArgs::plain: lda, ldx multiples of
+// 16 doubles, 128-B aligned bases), since a line shared with a neighbouring tile could be
+// cached by a reader of that neighbour before this tile was written.  Every wait also watches
+// the problem's abort word (non-PD pivot) and a poll budget, so no path can spin forever; a
+// spent budget is reported as info = -1 by the last workgroup to leave the launch.
 // ------------------------------------------------------------------------------------------
 constexpr int kPPMaxN = 240;          // schedule_kernel: one thread per key (4N+63 <= 1024)
 constexpr int kTChain = 0, kTL = 1, kTDP = 2, kTSP = 3, kTX = 4;
-constexpr long long kPollBudget = 1ll << 22;   // s_sleep polls before a wait gives up
+constexpr long long kPollBudget = 1ll << 22;   // default s_sleep polls before a wait gives up
+// gp_set_poll_budget (test / diagnostics hook): polls per wait for later launches; < 0 starts
+// every problem aborted (the deterministic abort path of the tests)
+long long g_poll_budget = kPollBudget;
+#ifdef GPFIT_PP_TRACE
+int* g_trace_dbg = nullptr;         // gp_pp_trace_set (trace build only)
+long long* g_trace_buf = nullptr;
+#endif
 
 __shared__ double g_keep[NB * LP];    // chain: L_j+1,j as [p][r] (opA layout) between steps
 __shared__ int g_msg[4];              // dequeued task / wait results broadcast to the workgroup
-__shared__ long long g_stall;         // debug trace only: ticks thread 0 spent polling flags
 
 struct PPArgs {
   double* A; long long sA; int lda;
   double* X; long long sX; int ldx;   // L^-1 (inv) or the 64 x 64N D_k scratch (plain)
   int n, N, batch, inv;
+  int plain;                          // produced tiles may be read with plain loads (above)
+  long long budget;                   // polls per wait
   int* info; double* logdet;
   const int2* tasks; int ntasks;
-  int* head;
+  int* head;                          // [0] dequeue counter, [1] workgroups that have left
   int* flags; int fstride;            // per problem: FL[N*N], FX[N*N], DPF[N], SPF[N], abort
-  int* dbg;                           // debug only: per-workgroup progress words (host memory)
-  long long* trace;                   // debug only: per-task / per-chain-step timestamps
+#ifdef GPFIT_PP_TRACE
+  int* dbg;                           // trace build only: per-workgroup progress words
+  long long* trace;                   // trace build only: per-task / per-chain-step stamps
+#endif
 };
 
 GP_DEV long long pp_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+#ifdef GPFIT_PP_TRACE
+// Diagnostics build only (libgpfit_trace.so, tools/dbg/pp_trace.py): timestamps per task and
+// chain phase, progress words per workgroup.  The shipped library has none of this.
+__shared__ long long g_stall;         // ticks thread 0 spent polling flags in the current task
+constexpr int kPPTraceSlots = 6;      // per task: wg|stall<<8, start, K-loop end, end, kind, i|j
 #define PP_TRACE(P, idx, val)                                                            \
   do {                                                                                   \
     if ((P).trace && threadIdx.x == 0) (P).trace[(idx)] = (val);                         \
   } while (0)
-
 #define PP_MARK(P, code, val)                                                            \
   do {                                                                                   \
     if ((P).dbg && threadIdx.x == 0) {                                                   \
@@ -948,6 +968,23 @@ GP_DEV long long pp_now() { return (long long)__builtin_amdgcn_s_memrealtime(); 
                          __HIP_MEMORY_SCOPE_SYSTEM);                                     \
     }                                                                                    \
   } while (0)
+#define PP_STALL_ADD(x) (g_stall += (x))
+#define PP_STALL_RESET() do { if (threadIdx.x == 0) g_stall = 0; } while (0)
+#define PP_STALL() g_stall
+#else
+#define PP_TRACE(P, idx, val) do { } while (0)
+#define PP_MARK(P, code, val) do { } while (0)
+#define PP_STALL_ADD(x) ((void)(x))
+#define PP_STALL_RESET() do { } while (0)
+#define PP_STALL() 0ll
+#endif
+
+// Give up problem `abort` after a spent poll budget (2), unless it already failed on a pivot.
+GP_DEV void pp_give_up(int* abort) {
+  int expected = 0;
+  __hip_atomic_compare_exchange_strong(abort, &expected, 2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+}
 
 GP_DEV __amdgpu_buffer_rsrc_t pp_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
@@ -1105,17 +1142,17 @@ GP_DEV void acc_to_lds_rm(double* Cs, const f64x4 (&acc)[2][2]) {
 
 // Wait until the flag *f is set, or the problem aborted / the poll budget ran out (then
 // false).  One lane polls; the verdict is broadcast through g_msg (all threads call).
-GP_DEV bool pp_wait1(const int* f, int* abort) {
+GP_DEV bool pp_wait1(const int* f, int* abort, long long budget) {
   if (threadIdx.x == 0) {
-    int ok = 0;
+    int ok = pp_ldflag(f) != 0;
     const long long ts = pp_now();
-    for (long long it = 0; it < kPollBudget; ++it) {
-      if (pp_ldflag(f)) { ok = 1; break; }
+    for (long long it = 0; !ok && it < budget; ++it) {
       if (pp_ldflag(abort)) break;
       __builtin_amdgcn_s_sleep(2);
+      ok = pp_ldflag(f) != 0;
     }
-    g_stall += pp_now() - ts;
-    if (!ok && !pp_ldflag(abort)) pp_stflag(abort, 2);   // budget spent: give up the problem
+    PP_STALL_ADD(pp_now() - ts);
+    if (!ok) pp_give_up(abort);   // budget spent (or aborted): give up the problem
     g_msg[1] = ok;
   }
   __syncthreads();
@@ -1160,8 +1197,9 @@ GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
   // L tiles (r, k) with r - k <= 1 pass through P partial sums in place (DP / SP tasks on any
   // XCD) before the chain writes L: read them with sc1 so no XCD's L2 serves a stale line.  Every
   // other operand tile is written once, by the XCD that alone read its old contents, and is
-  // only read after its flag: plain loads, cached in each reader's L2.
-  auto hz = [&](int r, int k) { return r - k <= 1; };
+  // only read after its flag: plain loads, cached in each reader's L2 -- when P.plain says no
+  // cache line spans two tiles (section comment), else sc1 as well.
+  auto hz = [&](int r, int k) { return r - k <= 1 || !P.plain; };
   if (T.kind == kTL || T.kind == kTSP) {   // L_ik L_jk^T with (i, j) = (T.i, T.j)
     u.a = atile(T.i, t);  u.fa = F + T.i * N + t;  u.av = rv(T.i);  u.ca = hz(T.i, t);
     u.b = atile(T.j, t);  u.fb = F + T.j * N + t;  u.bv = rv(T.j);  u.cb = hz(T.j, t);
@@ -1171,7 +1209,7 @@ GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
   } else {                                 // XT: L_ik X_kc, k = c + t (X_cc = D_c)
     const int k = T.j + t;
     u.a = atile(T.i, k);  u.fa = F + T.i * N + k;  u.av = rv(T.i);  u.ca = hz(T.i, k);
-    u.cb = false;
+    u.cb = !P.plain;
     u.b = Xb + k * NB + (long long)T.j * NB * P.ldx;
     u.ldb_ = P.ldx;
     u.fb = (k == T.j) ? F + k * N + k : F + N * N + k * N + T.j;
@@ -1188,7 +1226,7 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
     const int lane = threadIdx.x;
     int res = -1;
     const long long ts = pp_now();
-    for (long long it = 0; it < kPollBudget; ++it) {
+    for (long long it = 0;; ++it) {
       const int t = t0 + lane;
       bool rdy = true;
       if (t < T.nterms) {
@@ -1199,12 +1237,12 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
       const int lead = (~m == 0ull) ? 64 : __builtin_ctzll(~m);
       const int cnt = min(lead, T.nterms - t0);
       if (cnt > 0) { res = cnt; break; }
-      if (pp_ldflag(abort)) break;
+      if (it >= P.budget || pp_ldflag(abort)) break;
       __builtin_amdgcn_s_sleep(2);
     }
-    if (res < 0 && lane == 0 && !pp_ldflag(abort)) pp_stflag(abort, 2);
+    if (res < 0 && lane == 0) pp_give_up(abort);
     if (lane == 0) g_msg[2] = res;
-    if (lane == 0) g_stall += pp_now() - ts;
+    if (lane == 0) PP_STALL_ADD(pp_now() - ts);
   }
   __syncthreads();
   const int r = g_msg[2];
@@ -1301,8 +1339,12 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   double* Ab = P.A + T.b * P.sA;
   f64x4 acc[2][2];
   PP_MARK(P, 20 + T.kind, T.i * 1000 + T.j);
-  if (threadIdx.x == 0) g_stall = 0;
-  PP_TRACE(P, (long long)T.idx * 4 + 1, pp_now());
+  PP_STALL_RESET();
+  const long long tr = (long long)T.idx * 6;   // trace slots of this task (trace build)
+  (void)tr;
+  PP_TRACE(P, tr + 1, pp_now());
+  PP_TRACE(P, tr + 4, T.kind | (T.b << 4));
+  PP_TRACE(P, tr + 5, T.i | (T.j << 16));
   auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
   auto rv = [&](int r) { return min(NB, P.n - r * NB); };
   // the task's own A tile (DP / SP: the chain's partial-sum tile; LT: A_ij), in flight from
@@ -1312,9 +1354,9 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   if (T.kind != kTX) pp_load(ta, atile(ar, T.j), P.lda, rv(ar), T.kind == kTL ? NB : rv(T.j));
   if (!pp_accumulate(P, T, acc, abort)) return;
   PP_MARK(P, 30 + T.kind, T.i * 1000 + T.j);
-  PP_TRACE(P, (long long)T.idx * 4 + 2, pp_now());
+  PP_TRACE(P, tr + 2, pp_now());
   // slot 0: workgroup | ticks polled before the K loop finished << 8
-  PP_TRACE(P, (long long)T.idx * 4 + 0, blockIdx.x | (g_stall << 8));
+  PP_TRACE(P, tr + 0, blockIdx.x | (PP_STALL() << 8));
   if (T.kind == kTDP || T.kind == kTSP) {
     // partial sums for the chain, in place in A
     const int r = ar;
@@ -1322,14 +1364,14 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
     pp_sub_tile(ta, rv(r), rv(T.j), T.kind == kTDP, acc);
     pp_store_cm(dst, P.lda, sm.As, rv(r), rv(T.j), false, T.kind == kTDP);
     pp_publish(T.kind == kTDP ? F + 2 * N * N + T.j : F + 2 * N * N + N + T.j);
-    PP_TRACE(P, (long long)T.idx * 4 + 3, pp_now());
+    PP_TRACE(P, tr + 3, pp_now());
     return;
   }
   if (T.kind == kTL) {
     // L_ij = (A_ij - acc) D_j^T
     double* dst = atile(T.i, T.j);
     pp_sub_tile(ta, rv(T.i), NB, false, acc);
-    if (!pp_wait1(F + T.j * N + T.j, abort)) return;
+    if (!pp_wait1(F + T.j * N + T.j, abort, P.budget)) return;
     int ldd;
     const double* D = pp_dptr(P, T.b, T.j, ldd);
     OpTile td;
@@ -1342,13 +1384,13 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
     __syncthreads();
     pp_store_cm(dst, P.lda, sm.As, rv(T.i), NB, false);
     pp_publish(F + T.i * N + T.j);
-    PP_TRACE(P, (long long)T.idx * 4 + 3, pp_now());
+    PP_TRACE(P, tr + 3, pp_now());
     return;
   }
   // XT: X_ic = -D_i S, S = acc
   __syncthreads();
   acc_to_lds_rm(sm.Bs, acc);                            // Bs[p][cc] = S[p][cc]
-  if (!pp_wait1(F + T.i * N + T.i, abort)) return;
+  if (!pp_wait1(F + T.i * N + T.i, abort, P.budget)) return;
   PP_MARK(P, 40, T.i * 1000 + T.j);
   int ldd;
   const double* D = pp_dptr(P, T.b, T.i, ldd);
@@ -1364,7 +1406,7 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   pp_store_cm(Xb + T.i * NB + (long long)T.j * NB * P.ldx, P.ldx, sm.As, NB, NB, true);
   pp_publish(F + N * N + T.i * N + T.j);
   PP_MARK(P, 41, T.i * 1000 + T.j);
-  PP_TRACE(P, (long long)T.idx * 4 + 3, pp_now());
+  PP_TRACE(P, tr + 3, pp_now());
 }
 
 // The chain of problem b (see the section comment).
@@ -1381,13 +1423,14 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
   for (int j = 0; j < N; ++j) {
     const int nb = min(NB, P.n - j * NB);
     PP_MARK(P, 10, j);
-    const long long tb0 = (long long)P.ntasks * 4 + ((long long)b * N + j) * 8;
+    const long long tb0 = (long long)P.ntasks * 6 + ((long long)b * N + j) * 8;
+    (void)tb0;
     PP_TRACE(P, tb0 + 0, pp_now());
     // (a) C_jj = P_jj - L_j,j-1 L_j,j-1^T into As as a full symmetric [row][col] tile.  The
     // P_jj loads (16-B sc1, the whole tile; only its lower triangle is used) are in flight
     // during the SYRK.
     if (!pref) {
-      if (j >= 2 && !pp_wait1(F + 2 * N * N + j, abort)) return;
+      if (j >= 2 && !pp_wait1(F + 2 * N * N + j, abort, P.budget)) return;
       pp_load(tpj, atile(j, j), P.lda, nb, nb);
     }
     PP_TRACE(P, tb0 + 1, pp_now());
@@ -1442,7 +1485,7 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
     // (c) L_j+1,j = P_j+1,j D_j^T
     PP_MARK(P, 13, j);
     const int nb1 = min(NB, P.n - (j + 1) * NB);
-    if (j >= 1 && !pp_wait1(F + 2 * N * N + N + j, abort)) return;
+    if (j >= 1 && !pp_wait1(F + 2 * N * N + N + j, abort, P.budget)) return;
     PP_TRACE(P, tb0 + 5, pp_now());
     OpTile tp;
     pp_load(tp, atile(j + 1, j), P.lda, nb1, NB);      // As[p][r] = P[r][p]
@@ -1470,15 +1513,19 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
   if (threadIdx.x == 0 && P.logdet) P.logdet[b] = ld_sum;
 }
 
-// Chain wrapper: a poll budget spent anywhere in problem b (abort word 2) is reported as
-// info[b] = -1 (an internal error, never a pivot).
-GP_DEV void pp_chain_run(const PPArgs& P, int b) {
-  pp_chain(P, b);
-  if (threadIdx.x == 0) {
-    int* abort = P.flags + (long long)b * P.fstride + 2 * P.N * P.N + 2 * P.N;
-    if (pp_ldflag(abort) == 2 && P.info) P.info[b] = -1;
+// The last workgroup to leave the launch (every task, chain and XT alike, has returned by then)
+// reports a poll budget spent anywhere in problem b (abort word 2) as info[b] = -1: an internal
+// error, never a pivot.  The acq_rel exit count orders every workgroup's abort / info stores
+// before the reading workgroup's loads.
+GP_DEV void pp_exit(const PPArgs& P) {
+  if (threadIdx.x != 0) return;
+  const int done = __hip_atomic_fetch_add(P.head + 1, 1, __ATOMIC_ACQ_REL,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+  if (done != (int)gridDim.x - 1 || !P.info) return;
+  for (int b = 0; b < P.batch; ++b) {
+    const int* ab = P.flags + (long long)b * P.fstride + 2 * P.N * P.N + 2 * P.N;
+    if (pp_ldflag(ab) == 2) P.info[b] = -1;
   }
-  __syncthreads();
 }
 
 __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
@@ -1487,9 +1534,15 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
     __syncthreads();
     const int t = g_msg[0];
     __syncthreads();
+#ifdef GPFIT_PP_TRACE
     if (P.dbg && threadIdx.x == 0)
       __hip_atomic_store(P.dbg + blockIdx.x * 4, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (t >= P.ntasks) { PP_MARK(P, 99, 0); return; }
+#endif
+    if (t >= P.ntasks) {
+      PP_MARK(P, 99, 0);
+      pp_exit(P);
+      return;
+    }
     const int2 e = P.tasks[t];
     PPTask T;
     T.kind = e.x & 15;
@@ -1497,7 +1550,8 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
     T.i = e.y & 0xffff;
     T.j = e.y >> 16;
     if (T.kind == kTChain) {
-      pp_chain_run(P, T.b);
+      pp_chain(P, T.b);
+      __syncthreads();
       continue;
     }
     T.idx = t;
@@ -1563,11 +1617,14 @@ GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, int xd, F&& f) {
 GP_HD inline int pp_nkeys(int N, int lead, int xd) { return 4 * N - 1 + 4 * (lead + xd); }
 
 // Also zeroes the launch's flag words (dequeue head + per-tile flags) and info / logdet (in
-// place of three memset launches ahead of it: ~30 us of a C3 step).
+// place of three memset launches ahead of it: ~30 us of a C3 step); `preset_abort` (the
+// gp_set_poll_budget test hook) then marks every problem as having spent its poll budget.
 __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, int batch,
                                                            int inv, int lead, int xd,
                                                            int* zero, long long nzero,
-                                                           int* info, double* logdet) {
+                                                           int* info, double* logdet,
+                                                           int* flags, int fstride,
+                                                           int preset_abort) {
   __shared__ int cnt[2][1024];
   const int T = threadIdx.x;
   for (long long q = T; q < nzero; q += blockDim.x) zero[q] = 0;
@@ -1586,6 +1643,9 @@ __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, i
     __syncthreads();
     src ^= 1;
   }
+  if (preset_abort)   // after the barriers above: the zeroing is complete
+    for (int b = T; b < batch; b += blockDim.x)
+      flags[(long long)b * fstride + 2 * N * N + 2 * N] = 2;
   for (int b = T; b < batch; b += blockDim.x) tasks[b] = make_int2(kTChain | (b << 4), 0);
   if (T >= nk) return;
   const int excl = cnt[src][T] - own;
@@ -1669,57 +1729,103 @@ static int num_cus() {
   return ncu;
 }
 
-// Dequeue lead (see pp_schedule_kernel): W = kPPLead while every problem's chain and blocked
-// early tasks leave a worker free, else the topological order (W = 0).
-static int pp_lead(int batch, int grid) {
-  return (long long)batch * (kPPLeadBlocked + 1) < grid ? kPPLead : 0;
+// pp_kernel workgroups that can be resident at once on `stream`: its occupancy (1 per CU) x
+// the CUs the stream's CU mask enables.  The dequeue lead and the eligibility test are bounded
+// by this, not by the launched grid: a workgroup that is launched but never resident cannot
+// take a task.
+static int pp_resident(hipStream_t stream) {
+  static const int occ = [] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, pp_kernel, 256, 0) != hipSuccess ||
+        o <= 0)
+      o = 1;
+    return o;
+  }();
+  int cus = num_cus();
+  std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+  if (hipExtStreamGetCUMask(stream, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+    int on = 0;
+    for (uint32_t w : mask) on += __builtin_popcount(w);
+    if (on > 0 && on < cus) cus = on;
+  }
+  return occ * cus;
 }
 
-// The persistent dataflow factorisation (pp_kernel) on `stream`: stream-ordered scratch for the
-// task list, the dequeue head and the per-tile flags (hipMallocAsync / hipFreeAsync), one
-// schedule launch, one persistent launch with one workgroup per CU.  X is L^-1 (inv, zeroed by
-// the caller) or the 64 x 64N D_k scratch (ldx = 64).
-static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx, long long sX,
-                     int batch, int* info, double* logdet, bool inv, hipStream_t stream) {
+// Dequeue lead (see pp_schedule_kernel): W = kPPLead while every problem's chain and blocked
+// early tasks leave a resident worker free, else the topological order (W = 0).
+static int pp_lead(int batch, int resident) {
+  return (long long)batch * (kPPLeadBlocked + 1) < resident ? kPPLead : 0;
+}
+
+// Scratch of one persistent factorisation: the task list, a 256-B header (dequeue counter, exit
+// counter) and the per-problem flag words.
+struct PPScratch {
+  long long ntasks;
+  int fstride;
+  size_t task_bytes, flag_bytes;
+  size_t bytes() const { return task_bytes + flag_bytes; }
+};
+
+static PPScratch pp_scratch(int n, int batch, bool inv) {
+  PPScratch s;
   const int N = gp_ceil_div(n, NB);
-  const long long ntasks = pp_task_count(N, inv) * batch;
-  const int fstride = ((2 * N * N + 2 * N + 1 + 31) / 32) * 32;
-  const size_t task_bytes = ((size_t)ntasks * sizeof(int2) + 255) / 256 * 256;
-  const size_t flag_bytes = 256 + (size_t)batch * fstride * sizeof(int);
-  const int grid = (int)(ntasks < num_cus() ? ntasks : num_cus());
-  char* scr = nullptr;
-  GP_CK(hipMallocAsync(reinterpret_cast<void**>(&scr), task_bytes + flag_bytes, stream));
+  s.ntasks = pp_task_count(N, inv) * batch;
+  s.fstride = ((2 * N * N + 2 * N + 1 + 31) / 32) * 32;
+  s.task_bytes = ((size_t)s.ntasks * sizeof(int2) + 255) / 256 * 256;
+  s.flag_bytes = ((256 + (size_t)batch * s.fstride * sizeof(int)) + 255) / 256 * 256;
+  return s;
+}
+
+static bool pp_shape_ok(int n, int batch) {
+  const int N = gp_ceil_div(n, NB);
+  return N <= kPPMaxN && pp_task_count(N, true) * (long long)batch < (1ll << 30);
+}
+
+static bool pp_eligible(int n, int batch, int resident) {
+  // the chains hold `batch` workgroups for the whole launch: at least as many workers again
+  return pp_shape_ok(n, batch) && 2 * batch <= resident &&
+         std::getenv("GPFIT_POTRF_SWEEP") == nullptr;
+}
+
+// The persistent dataflow factorisation (pp_kernel) on `stream` in the caller's scratch `scr`
+// (pp_scratch bytes, 256-B aligned): one schedule launch, one persistent launch with one
+// workgroup per resident slot.  X is L^-1 (inv, zeroed by the caller) or the 64 x 64N D_k
+// scratch (ldx = 64).
+static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx, long long sX,
+                     int batch, int* info, double* logdet, bool inv, char* scr, int resident,
+                     hipStream_t stream) {
+  const int N = gp_ceil_div(n, NB);
+  const PPScratch s = pp_scratch(n, batch, inv);
+  const int grid = (int)(s.ntasks < resident ? s.ntasks : resident);
   int2* tasks = reinterpret_cast<int2*>(scr);
-  int* head = reinterpret_cast<int*>(scr + task_bytes);
-  int* flags = reinterpret_cast<int*>(scr + task_bytes + 256);
+  int* head = reinterpret_cast<int*>(scr + s.task_bytes);
+  int* flags = reinterpret_cast<int*>(scr + s.task_bytes + 256);
   const int lead = pp_lead(batch, grid);
+  const long long budget = g_poll_budget;
   // the schedule kernel also zeroes head + flags and info / logdet
   hipLaunchKernelGGL(pp_schedule_kernel, dim3(1), dim3(1024), 0, stream, tasks, N, batch,
-                     inv ? 1 : 0, lead, kPPXDelay, head, (long long)(flag_bytes / sizeof(int)),
-                     info, logdet);
+                     inv ? 1 : 0, lead, kPPXDelay, head, (long long)(s.flag_bytes / sizeof(int)),
+                     info, logdet, flags, s.fstride, budget < 0 ? 1 : 0);
   GP_CK(hipGetLastError());
   PPArgs P;
   P.A = A; P.sA = sA; P.lda = lda;
   P.X = X; P.sX = sX; P.ldx = ldx;
   P.n = n; P.N = N; P.batch = batch; P.inv = inv ? 1 : 0;
+  // plain (L2-cached) loads of produced tiles only when no 128-B line spans two tiles
+  auto al128 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 127) == 0; };
+  P.plain = (lda % 16 == 0) && (ldx % 16 == 0) && al128(A) && al128(X) &&
+            (batch == 1 || (sA % 16 == 0 && sX % 16 == 0));
+  P.budget = budget > 0 ? budget : kPollBudget;
   P.info = info; P.logdet = logdet;
-  P.tasks = tasks; P.ntasks = (int)ntasks;
-  P.head = head; P.flags = flags; P.fstride = fstride;
-  const char* dbg = std::getenv("GPFIT_PP_DEBUG_PTR");   // debug only: pinned host int[4*#CU]
-  P.dbg = dbg ? reinterpret_cast<int*>(std::strtoull(dbg, nullptr, 0)) : nullptr;
-  const char* trc = std::getenv("GPFIT_PP_TRACE_PTR");   // debug only: device int64 buffer
-  P.trace = trc ? reinterpret_cast<long long*>(std::strtoull(trc, nullptr, 0)) : nullptr;
+  P.tasks = tasks; P.ntasks = (int)s.ntasks;
+  P.head = head; P.flags = flags; P.fstride = s.fstride;
+#ifdef GPFIT_PP_TRACE
+  P.dbg = g_trace_dbg;
+  P.trace = g_trace_buf;
+#endif
   hipLaunchKernelGGL(pp_kernel, dim3(grid), dim3(256), 0, stream, P);
   GP_CK(hipGetLastError());
-  GP_CK(hipFreeAsync(scr, stream));
   return 0;
-}
-
-static bool pp_eligible(int n, int batch) {
-  const int N = gp_ceil_div(n, NB);
-  // the chains hold `batch` workgroups for the whole launch: at least as many workers again
-  return N <= kPPMaxN && pp_task_count(N, true) * (long long)batch < (1ll << 30) &&
-         2 * batch <= num_cus() && std::getenv("GPFIT_POTRF_SWEEP") == nullptr;
 }
 
 // Zero L^-1 (upper triangle + padding): one memset for a packed batch, else one 2-D memset per
@@ -1737,16 +1843,28 @@ static hipError_t zero_linv(double* Linv, int npad, int ldinv, long long strideI
   return hipSuccess;
 }
 
-extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double* Linv,
-                            int ldinv, long long strideInv, int batch, int* info,
-                            double* logdet, hipStream_t stream) {
-  return gpfit_potrf_inv_event(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,
-                               stream, -1, nullptr);
+static bool ws_aligned(const void* ws) { return (reinterpret_cast<uintptr_t>(ws) & 255) == 0; }
+
+long long gpfit_potrf_inv_ws_bytes(int n, int batch) {
+  if (n <= 0 || batch <= 0 || !pp_shape_ok(n, batch)) return 0;
+  return (long long)pp_scratch(n, batch, true).bytes();
 }
 
-int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
-                          int ldinv, long long strideInv, int batch, int* info, double* logdet,
-                          hipStream_t stream, int k_ev, hipEvent_t ev) {
+extern "C" long long gp_potrf_inv_ws_bytes(int n, int batch) {
+  if (n < 0 || batch < 0) return -1;
+  return gpfit_potrf_inv_ws_bytes(n, batch);
+}
+
+extern "C" long long gp_potrf_ws_bytes(int n, int batch) {
+  if (n < 0 || batch < 0) return -1;
+  if (n == 0 || batch == 0) return 0;
+  const long long sD = (long long)NB * gp_ceil_div(n, NB) * NB;
+  const long long d = ((8LL * sD * batch) + 255) / 256 * 256;
+  return d + (pp_shape_ok(n, batch) ? (long long)pp_scratch(n, batch, false).bytes() : 0);
+}
+
+static int potrf_inv_args(const double* A, int n, int lda, long long strideA, const double* Linv,
+                          int ldinv, long long strideInv, int batch) {
   if (!A) return -1;
   if (n < 0) return -2;
   if (lda < n || lda < 1) return -3;
@@ -1756,9 +1874,32 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
   if (ldinv < npad || ldinv < 1) return -6;
   if (batch > 1 && strideInv < (long long)ldinv * npad) return -7;
   if (batch < 0) return -8;
+  return 0;
+}
+
+static int potrf_args(const double* A, int n, int lda, long long strideA, int batch) {
+  if (!A) return -1;
+  if (n < 0) return -2;
+  if (lda < n || lda < 1) return -3;
+  if (batch > 1 && strideA < (long long)lda * n) return -4;
+  if (batch < 0) return -5;
+  return 0;
+}
+
+int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
+                          int ldinv, long long strideInv, int batch, int* info, double* logdet,
+                          void* ws, long long ws_bytes, hipStream_t stream, int k_ev,
+                          hipEvent_t ev) {
+  const int arc = potrf_inv_args(A, n, lda, strideA, Linv, ldinv, strideInv, batch);
+  if (arc) return arc;
   if (n == 0 || batch == 0) return 0;
-  const bool pp = pp_eligible(n, batch);
-  if (!pp) {   // (pp_factor's schedule kernel zeroes them)
+  const int npad = gp_padded_n(n);
+  const int resident = pp_resident(stream);
+  const bool pp = pp_eligible(n, batch, resident);
+  if (pp) {
+    if (!ws || !ws_aligned(ws)) return -11;
+    if (ws_bytes < gpfit_potrf_inv_ws_bytes(n, batch)) return -12;
+  } else {   // (pp_factor's schedule kernel zeroes them)
     if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
     if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
   }
@@ -1771,7 +1912,8 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
     // one asked for at k_ev >= N after it
     const int N = gp_ceil_div(n, NB);
     if (ev && k_ev >= 0 && k_ev < N) GP_CK(hipEventRecord(ev, stream));
-    rc = pp_factor(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet, true, stream);
+    rc = pp_factor(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet, true,
+                   static_cast<char*>(ws), resident, stream);
     if (rc == 0 && ev && !(k_ev >= 0 && k_ev < N)) GP_CK(hipEventRecord(ev, stream));
   } else {
     rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,
@@ -1781,29 +1923,69 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
   return rc;
 }
 
-extern "C" int gp_potrf(double* A, int n, int lda, long long strideA, int batch, int* info,
-                        double* logdet, hipStream_t stream) {
-  if (!A) return -1;
-  if (n < 0) return -2;
-  if (lda < n || lda < 1) return -3;
-  if (batch > 1 && strideA < (long long)lda * n) return -4;
-  if (batch < 0) return -5;
+extern "C" int gp_potrf_inv_ws(double* A, int n, int lda, long long strideA, double* Linv,
+                               int ldinv, long long strideInv, int batch, int* info,
+                               double* logdet, void* ws, long long ws_bytes,
+                               hipStream_t stream) {
+  return gpfit_potrf_inv_event(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,
+                               ws, ws_bytes, stream, -1, nullptr);
+}
+
+// The allocating forms: stream-ordered scratch (hipMallocAsync), freed behind the launches on
+// every path, including a failed launch.
+extern "C" int gp_potrf_inv(double* A, int n, int lda, long long strideA, double* Linv,
+                            int ldinv, long long strideInv, int batch, int* info,
+                            double* logdet, hipStream_t stream) {
+  const int arc = potrf_inv_args(A, n, lda, strideA, Linv, ldinv, strideInv, batch);
+  if (arc) return arc;
+  const long long bytes = (n > 0 && batch > 0) ? gpfit_potrf_inv_ws_bytes(n, batch) : 0;
+  void* ws = nullptr;
+  if (bytes > 0) GP_CK(hipMallocAsync(&ws, (size_t)bytes, stream));
+  const int rc = gp_potrf_inv_ws(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info,
+                                 logdet, ws, bytes, stream);
+  if (ws) {
+    const hipError_t e = hipFreeAsync(ws, stream);
+    if (rc == 0 && e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  }
+  return rc;
+}
+
+extern "C" int gp_potrf_ws(double* A, int n, int lda, long long strideA, int batch, int* info,
+                           double* logdet, void* ws, long long ws_bytes, hipStream_t stream) {
+  const int arc = potrf_args(A, n, lda, strideA, batch);
+  if (arc) return arc;
   if (n == 0 || batch == 0) return 0;
-  const bool pp = pp_eligible(n, batch);
+  if (!ws || !ws_aligned(ws)) return -8;
+  if (ws_bytes < gp_potrf_ws_bytes(n, batch)) return -9;
+  const int resident = pp_resident(stream);
+  const bool pp = pp_eligible(n, batch, resident);
   if (!pp) {   // (pp_factor's schedule kernel zeroes them)
     if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
     if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
   }
-  // D_k scratch: NB x (N NB) per problem, stream-ordered (freed when the sweep has run)
+  // D_k scratch: NB x (N NB) per problem at the head of ws, then the persistent scratch
   const int N = gp_ceil_div(n, NB);
   const long long sD = (long long)NB * N * NB;
-  double* D = nullptr;
-  GP_CK(hipMallocAsync(reinterpret_cast<void**>(&D), sizeof(double) * sD * batch, stream));
-  const int rc = pp
-      ? pp_factor(A, n, lda, strideA, D, NB, sD, batch, info, logdet, false, stream)
-      : potrf_sweep<kPotrf>(A, n, lda, strideA, D, NB, sD, batch, info, logdet, stream, -1,
-                            nullptr);
-  GP_CK(hipFreeAsync(D, stream));
+  double* D = static_cast<double*>(ws);
+  char* scr = static_cast<char*>(ws) + ((8LL * sD * batch) + 255) / 256 * 256;
+  return pp ? pp_factor(A, n, lda, strideA, D, NB, sD, batch, info, logdet, false, scr, resident,
+                        stream)
+            : potrf_sweep<kPotrf>(A, n, lda, strideA, D, NB, sD, batch, info, logdet, stream,
+                                  -1, nullptr);
+}
+
+extern "C" int gp_potrf(double* A, int n, int lda, long long strideA, int batch, int* info,
+                        double* logdet, hipStream_t stream) {
+  const int arc = potrf_args(A, n, lda, strideA, batch);
+  if (arc) return arc;
+  const long long bytes = (n > 0 && batch > 0) ? gp_potrf_ws_bytes(n, batch) : 0;
+  void* ws = nullptr;
+  if (bytes > 0) GP_CK(hipMallocAsync(&ws, (size_t)bytes, stream));
+  const int rc = gp_potrf_ws(A, n, lda, strideA, batch, info, logdet, ws, bytes, stream);
+  if (ws) {
+    const hipError_t e = hipFreeAsync(ws, stream);
+    if (rc == 0 && e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  }
   return rc;
 }
 
@@ -1835,4 +2017,27 @@ extern "C" int gp_trtri(const double* L, int n, int ldl, long long strideL, doub
   return potrf_sweep<kTrtri>(const_cast<double*>(L), n, ldl, strideL, Linv, ldinv, strideInv,
                              batch, info, nullptr, stream, -1, nullptr);
 }
+
+// Poll budget of the persistent factorisation's waits for later launches (process-wide test /
+// diagnostics hook): polls > 0 sets it, 0 restores the default, < 0 makes every later
+// factorisation start with its problems aborted (info = -1: the deterministic abort path).
+// Returns the previous setting.
+extern "C" long long gp_set_poll_budget(long long polls) {
+  const long long prev = g_poll_budget;
+  g_poll_budget = polls == 0 ? kPollBudget : polls;
+  return prev;
+}
+
+#ifdef GPFIT_PP_TRACE
+// Trace build only (libgpfit_trace.so): device buffers the next persistent launches fill.
+extern "C" int gp_pp_trace_set(void* dbg, void* trace) {
+  g_trace_dbg = static_cast<int*>(dbg);
+  g_trace_buf = static_cast<long long*>(trace);
+  return 0;
+}
+extern "C" long long gp_pp_trace_slots(int n, int batch) {
+  const int N = gp_ceil_div(n, NB);
+  return pp_scratch(n, batch, true).ntasks * kPPTraceSlots + (long long)batch * N * 8;
+}
+#endif
 #undef GP_CK

@@ -95,7 +95,10 @@ GP_DEV f64x4 zero4() { f64x4 z = {0.0, 0.0, 0.0, 0.0}; return z; }
 // literal operand), so no constant has to be re-materialised in a VGPR per call (ocml's fmac
 // form overwrites its constant registers: 22 extra v_mov per exp inside a loop).  a is clamped
 // to 1100 first: e^-1100 underflows to +0 through the ldexp, the only range check a
-// non-negative argument needs.  Accuracy: within 1 ulp of exp (the same reduction and
+// non-negative argument needs.  v_min_f64 drops a NaN operand (IEEE minNum), so the result is
+// finally passed through fma(a, 0, e): +0 for finite a (e unchanged), NaN for a NaN / Inf
+// distance (NaN or Inf beta / design values), so bad inputs reach the factorisation's info
+// instead of becoming a finite ~0.  Accuracy: within 1 ulp of exp (the same reduction and
 // polynomial as ocml).
 // fma(p, r, c) with c wave-uniform, pinned to VOP3 v_fma_f64 with c in an SGPR pair (the
 // compiler otherwise keeps c in a VGPR and copies it before every v_fmac_f64).
@@ -121,7 +124,7 @@ GP_DEV double exp_neg(double a) {
   p = fma_sc(p, r, 0x1.000000000000bp-1);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-  return __builtin_ldexp(p, (int)k);
+  return fma(a, 0.0, __builtin_ldexp(p, (int)k));
 }
 
 // Squared ARD distance sum_k beta_k (a_k - b_k)^2 ; D is a compile-time dimension bound.

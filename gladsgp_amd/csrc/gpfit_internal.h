@@ -12,12 +12,16 @@ hipError_t gpfit_trmv_launch(const double* Linv, int ld, long long sL, const dou
 
 constexpr int GPFIT_POTRF_NB = 64;   // column block of gp_potrf_inv (chol.hip NB)
 
-// gp_potrf_inv that also records `ev` on the stream once block step `k_ev` (NB = 64 columns)
-// has been enqueued (k_ev clamped to the last step); chol.hip.  Lets a caller start HBM-bound
-// side work only when the factorisation turns latency-bound.
+// gp_potrf_inv_ws that also records `ev` on the stream once block step `k_ev` (NB = 64
+// columns) has been enqueued (k_ev clamped to the last step); chol.hip.  Lets a caller start
+// HBM-bound side work only when the factorisation turns latency-bound.  `ws` (256-B aligned)
+// holds gpfit_potrf_inv_ws_bytes(n, batch) bytes: the persistent factorisation's task list and
+// flags (nothing when n is beyond the persistent kernel's range).
 int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
                           int ldinv, long long strideInv, int batch, int* info, double* logdet,
-                          hipStream_t stream, int k_ev, hipEvent_t ev);
+                          void* ws, long long ws_bytes, hipStream_t stream, int k_ev,
+                          hipEvent_t ev);
+long long gpfit_potrf_inv_ws_bytes(int n, int batch);
 
 // gp_gram_ardse writing only the lower triangle (j <= i); the upper triangle is left untouched.
 // For callers that factorise the result right away (gram.hip).

@@ -45,14 +45,16 @@ __global__ __launch_bounds__(1024) void trmv_kernel(const double* __restrict__ L
   }
 }
 
-// out[b] = sign * (1/2 ||z_b||^2 + 1/2 logdet[b]); a problem whose factorisation failed
-// (info[b] != 0, when info is given) gets sign * +inf.
+// out[b] = sign * (1/2 ||z_b||^2 + 1/2 logdet[b]); a problem whose matrix is not positive
+// definite (info[b] > 0, when info is given) gets sign * +inf, a factorisation that gave up
+// (info[b] < 0, an internal error) NaN and raises the sticky `status` word (when given).
 __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restrict__ z, int ldz,
                                                          int n,
                                                          const double* __restrict__ logdet,
                                                          const int* __restrict__ info,
                                                          double sign,
-                                                         double* __restrict__ nll) {
+                                                         double* __restrict__ nll,
+                                                         int* __restrict__ status) {
   const int b = blockIdx.x;
   const double* zb = z + (long long)b * ldz;
   double acc = 0.0;
@@ -64,7 +66,10 @@ __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restric
   __syncthreads();
   if (threadIdx.x == 0) {
     const double v = 0.5 * ((red[0] + red[1]) + (red[2] + red[3])) + 0.5 * logdet[b];
-    nll[b] = sign * ((info && info[b] != 0) ? __builtin_huge_val() : v);
+    const int f = info ? info[b] : 0;
+    nll[b] = f < 0 ? __builtin_nan("") : sign * (f > 0 ? __builtin_huge_val() : v);
+    if (f < 0 && status)
+      __hip_atomic_fetch_or(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -119,7 +124,7 @@ extern "C" int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
   hipError_t e = gpfit_trmv_launch(Linv, ldinv, strideInv, w, ldw, work, n, n, n, batch, stream);
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   hipLaunchKernelGGL(nll_reduce_kernel, dim3(batch), dim3(256), 0, stream, work, n, n, logdet,
-                     (const int*)nullptr, 1.0, nll);
+                     (const int*)nullptr, 1.0, nll, (int*)nullptr);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }
@@ -131,6 +136,9 @@ struct LoglikWs {
   double* z;
   double* logdet;
   int* info;
+  int* status;       // sticky internal-error word (gp_loglik_status)
+  char* pot;         // the factorisation's scratch
+  long long pot_bytes;
   long long bytes;
 };
 
@@ -150,6 +158,11 @@ LoglikWs loglik_carve(void* ws, int n, int batch) {
   off += up(8LL * batch);
   w.info = reinterpret_cast<int*>(p + off);
   off += up(4LL * batch);
+  w.status = reinterpret_cast<int*>(p + off);
+  off += 256;
+  w.pot = p + off;
+  w.pot_bytes = gpfit_potrf_inv_ws_bytes(n, batch);
+  off += up(w.pot_bytes);
   w.bytes = off;
   return w;
 }
@@ -176,7 +189,7 @@ extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* b
   if (ldw < n && batch > 1) return -10;
   if (batch < 0) return -11;
   if (n == 0 || batch == 0) return 0;
-  if (!ws) return -12;
+  if (!ws || (reinterpret_cast<uintptr_t>(ws) & 255)) return -12;
   const LoglikWs c = loglik_carve(ws, n, batch);
   if (ws_bytes < c.bytes) return -13;
   if (!ll) return -14;
@@ -184,14 +197,14 @@ extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* b
   int rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, c.G, n, (long long)n * n,
                             batch, stream);
   if (rc) return rc;
-  rc = gp_potrf_inv(c.G, n, n, (long long)n * n, c.Linv, npad, (long long)npad * npad, batch,
-                    c.info, c.logdet, stream);
+  rc = gpfit_potrf_inv_event(c.G, n, n, (long long)n * n, c.Linv, npad, (long long)npad * npad,
+                             batch, c.info, c.logdet, c.pot, c.pot_bytes, stream, -1, nullptr);
   if (rc) return rc;
   hipError_t e = gpfit_trmv_launch(c.Linv, npad, (long long)npad * npad, w, ldw, c.z, n, n, n,
                                    batch, stream);
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   hipLaunchKernelGGL(nll_reduce_kernel, dim3(batch), dim3(256), 0, stream, c.z, n, n, c.logdet,
-                     (const int*)c.info, -1.0, ll);
+                     (const int*)c.info, -1.0, ll, c.status);
   e = hipGetLastError();
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   if (info) {
@@ -199,4 +212,18 @@ extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* b
     if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   }
   return 0;
+}
+
+extern "C" int gp_loglik_status(void* ws, int n, int batch, int reset, hipStream_t stream) {
+  if (!ws) return -1;
+  if (n < 0) return -2;
+  if (batch < 0) return -3;
+  if (n == 0 || batch == 0) return 0;
+  const LoglikWs c = loglik_carve(ws, n, batch);
+  int host = 0;
+  hipError_t e = hipMemcpyAsync(&host, c.status, sizeof(int), hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess && reset) e = hipMemsetAsync(c.status, 0, sizeof(int), stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  return host ? GPFIT_ERR_INTERNAL : 0;
 }

@@ -342,14 +342,16 @@ __global__ __launch_bounds__(256) void trmv_sum_kernel(const double* __restrict_
 
 struct Plan {
   int npad, NI, mc, NC, nchunks, slabs;
-  long long off_z, off_zp, off_kt, off_part, bytes, slab_elems, part_elems;
+  long long off_z, off_zp, off_kt, off_part, off_pot, bytes, slab_elems, part_elems;
 };
 
 // slabs = 1: one cross-covariance chunk and one partial-sum slab at a time (gp_predict, which
 // finalises each chunk after its TRMM); slabs = nchunks: every chunk's cross-covariance and
 // partial sums materialised (gp_predict_cross + gp_predict_solve, gp_fit_predict), so one
-// finalize launch after the last TRMM covers all m points.
-Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
+// finalize launch after the last TRMM covers all m points.  `potrf`: plus the factorisation's
+// scratch (gp_fit_predict).
+Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false,
+               bool potrf = false) {
   Plan p;
   p.npad = gp_padded_n(n);
   p.NI = p.npad / BI;
@@ -385,7 +387,8 @@ Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false) {
   p.off_zp = ((z * 8 + 255) / 256) * 256;
   p.off_kt = p.off_zp + ((zp * 8 + 255) / 256) * 256;
   p.off_part = p.off_kt + ((kt * 8 + 255) / 256) * 256;
-  p.bytes = p.off_part + part * 8;
+  p.off_pot = ((p.off_part + part * 8 + 255) / 256) * 256;
+  p.bytes = p.off_pot + (potrf ? gpfit_potrf_inv_ws_bytes(n, batch) : 0);
   return p;
 }
 
@@ -403,7 +406,7 @@ extern "C" long long gp_predict_prepared_ws_bytes(int n, int m, int batch, int m
 
 extern "C" long long gp_fit_predict_ws_bytes(int n, int m, int batch, int m_chunk) {
   if (n <= 0 || m <= 0 || batch <= 0) return 0;
-  return make_plan(n, m, batch, m_chunk, true).bytes;
+  return make_plan(n, m, batch, m_chunk, true, true).bytes;
 }
 
 namespace {
@@ -442,12 +445,14 @@ int check_solve(const double* Linv, int ldinv, long long strideInv, int n, const
 
 struct WS {
   double *z, *zp, *kt, *part;
+  char* pot;
 };
 
 WS carve(const Plan& p, void* ws) {
   char* base = static_cast<char*>(ws);
   return {reinterpret_cast<double*>(base + p.off_z), reinterpret_cast<double*>(base + p.off_zp),
-          reinterpret_cast<double*>(base + p.off_kt), reinterpret_cast<double*>(base + p.off_part)};
+          reinterpret_cast<double*>(base + p.off_kt), reinterpret_cast<double*>(base + p.off_part),
+          base + p.off_pot};
 }
 
 // z = L^-1 w into w.z (npad rows per problem), two passes through w.zp (the same arithmetic
@@ -719,8 +724,8 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   if (ldg < n || (batch > 1 && strideG < (long long)ldg * n)) return -26;
   if (n == 0 || m == 0 || batch == 0) return 0;
   if (m_chunk < 0) return -23;
-  const Plan p = make_plan(n, m, batch, m_chunk, true);
-  if (!ws) return -21;
+  const Plan p = make_plan(n, m, batch, m_chunk, true, true);
+  if (!ws || (reinterpret_cast<uintptr_t>(ws) & 255)) return -21;
   if (ws_bytes < p.bytes) return -22;
   const WS w = carve(p, ws);
   gp_ctx_s* S = static_cast<gp_ctx_s*>(ctx);
@@ -747,7 +752,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   const int k_late = S ? (int)(S->cross_start * nblk) : -1;
   if (S && k_late <= 0) GP_CK(hipEventRecord(S->e_late, fact));
   rc = gpfit_potrf_inv_event(G, n, ldg, strideG, Linv, ldinv, strideInv, batch, info, logdet,
-                             fact, k_late > 0 ? k_late : -1,
+                             w.pot, p.bytes - p.off_pot, fact, k_late > 0 ? k_late : -1,
                              (S && k_late > 0) ? S->e_late : nullptr);
   if (rc) return rc;
   if (S) {

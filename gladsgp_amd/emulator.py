@@ -282,10 +282,12 @@ def gp_params(samples, LamSim, d, P, pred_nugget=True):
 
 
 def predict_units(X, Xs, w_units, beta_u, s_u, delta_u, sp_u, budget_bytes=2 << 30,
-                  m_chunk=0):
+                  m_chunk=0, group=None):
     """Posterior mean / variance of a list of GPs sharing X and Xs: returns (U, m) x 2.
 
-    Units are processed in groups bounded by ``budget_bytes`` of Gram + L^-1 storage.
+    Units are processed in groups bounded by ``budget_bytes`` of Gram + L^-1 storage, and by
+    ``group`` GPs per group when given (each group is one batched Gram -> factorisation ->
+    prediction).
     """
     dev = X.device
     U = beta_u.shape[0]
@@ -294,6 +296,8 @@ def predict_units(X, Xs, w_units, beta_u, s_u, delta_u, sp_u, budget_bytes=2 << 
     npad = kernels.padded_n(n)
     per = 8 * (n * n + npad * npad)
     g = max(1, int(budget_bytes // per))
+    if group is not None:
+        g = max(1, min(g, int(group)))
     mean = torch.empty((U, m), dtype=F64, device=dev)
     var = torch.empty((U, m), dtype=F64, device=dev)
     ws = kernels.PredictWorkspace()
@@ -311,14 +315,21 @@ def predict_units(X, Xs, w_units, beta_u, s_u, delta_u, sp_u, budget_bytes=2 << 
 class EmulatorPrediction:
     """Predictions of the P PC-GPs for each posterior sample at ``t_pred`` (m x d).
 
-    ``ctx`` (a :class:`gladsgp_amd.dist.Context`) shards the (sample, PC) units round-robin
-    over ranks; rank 0 receives the gathered (S, m, P) results, other ranks hold ``None``.
+    ``ctx`` (a :class:`gladsgp_amd.dist.Context`) shards the work over ranks; rank 0 receives
+    the gathered (S, m, P) results, other ranks hold ``None``:
+      * units (S P) >= ranks: the (sample, PC) units are dealt round-robin (SURVEY §8e,
+        multivariate emulator);
+      * fewer units than ranks (the reference's scalar GPs: P = 1 with few samples,
+        fit_scalar_models.py:477-481, mean_response.py:114-126) with m >= ranks: the test points
+        are split instead, every rank predicting every unit on its contiguous block
+        (``shard="points"``, SURVEY §8e single-output GP; see gladsgp_amd.sharded).
+    ``shard`` forces "units" or "points".  ``group`` caps the GPs per batched factorisation.
     """
 
     def __init__(self, model: EmulatorModel = None, samples: dict = None, t_pred=None,
                  pred_nugget: bool = True, ctx: gdist.Context | None = None,
                  budget_bytes: int = 2 << 30, m_chunk: int = 0, realize: bool = False,
-                 seed: int | None = None):
+                 seed: int | None = None, group: int | None = None, shard: str | None = None):
         if model is None or samples is None or t_pred is None:
             raise ValueError("EmulatorPrediction needs model, samples and t_pred")
         self.model = model
@@ -332,27 +343,47 @@ class EmulatorPrediction:
         self.S, self.m, self.P = S, Xs.shape[0], P
         self.lamWOs = np.asarray(samples["lamWOs"], dtype=np.float64).reshape(S)
         units = [(a, j) for a in range(S) for j in range(P)]
-        rank, world = (ctx.rank, ctx.world) if ctx is not None else (0, 1)
-        mine = gdist.shard_units(len(units), rank, world)
+        dist_on = ctx is not None and ctx.distributed
+        rank, world = (ctx.rank, ctx.world) if dist_on else (0, 1)
+        if shard is None:
+            shard = "points" if (dist_on and len(units) < world and self.m >= world) else "units"
+        if shard not in ("units", "points"):
+            raise ValueError(f"shard must be 'units' or 'points', got {shard!r}")
+        self.shard = shard if dist_on else "units"
         w_hat = model.w_hat.transpose(0, 1).contiguous()       # (P, n)
-        if mine:
-            sel_s = np.array([units[u][0] for u in mine])
-            sel_j = np.array([units[u][1] for u in mine])
-            t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=F64, device=dev)  # noqa
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=F64, device=dev)  # noqa
+        if self.shard == "points":
+            # every unit on this rank's contiguous block of the test points
+            lo, hi = gdist.shard_range(self.m, rank, world)
+            sel_s = np.array([u[0] for u in units])
+            sel_j = np.array([u[1] for u in units])
             jj = torch.as_tensor(sel_j, device=dev)
-            mean_l, var_l = predict_units(X, Xs, w_hat[jj].contiguous(),
+            mean_l, var_l = predict_units(X, Xs[lo:hi].contiguous(), w_hat[jj].contiguous(),
                                           t(beta[sel_s, sel_j]), t(s[sel_s, sel_j]),
                                           t(delta[sel_s, sel_j]), t(sp[sel_s, sel_j]),
-                                          budget_bytes, m_chunk)
+                                          budget_bytes, m_chunk, group)
         else:
-            mean_l = torch.empty((0, self.m), dtype=F64, device=dev)
-            var_l = torch.empty((0, self.m), dtype=F64, device=dev)
+            mine = gdist.shard_units(len(units), rank, world)
+            if mine:
+                sel_s = np.array([units[u][0] for u in mine])
+                sel_j = np.array([units[u][1] for u in mine])
+                jj = torch.as_tensor(sel_j, device=dev)
+                mean_l, var_l = predict_units(X, Xs, w_hat[jj].contiguous(),
+                                              t(beta[sel_s, sel_j]), t(s[sel_s, sel_j]),
+                                              t(delta[sel_s, sel_j]), t(sp[sel_s, sel_j]),
+                                              budget_bytes, m_chunk, group)
+            else:
+                mean_l = torch.empty((0, self.m), dtype=F64, device=dev)
+                var_l = torch.empty((0, self.m), dtype=F64, device=dev)
         self.ctx = ctx
         self.realized = bool(realize)
         self.seed = int(np.random.SeedSequence().entropy & (2 ** 63 - 1)) if seed is None \
             else int(seed)
         self._w_dtype = np.dtype(np.float64)
-        both = assemble_units(ctx, mean_l, var_l, len(units))
+        if self.shard == "points":
+            both = assemble_points(ctx, mean_l, var_l, self.m)
+        else:
+            both = assemble_units(ctx, mean_l, var_l, len(units))
         if both is None:
             self.mean_dev = self.w_dev = self.var_dev = None
             return
@@ -488,6 +519,19 @@ def assemble_units(ctx, mean_l: torch.Tensor, var_l: torch.Tensor, n_units: int)
         return None
     allb = unit_order(allb, n_units, world)
     return allb[:, 0], allb[:, 1]
+
+
+def assemble_points(ctx, mean_l: torch.Tensor, var_l: torch.Tensor, m: int):
+    """Gather every rank's (U, m_r) test-point block of all units to rank 0 as (U, m) x 2
+    (one gather; None on the other ranks)."""
+    if ctx is None or not ctx.distributed:
+        return mean_l, var_l
+    counts = [b - a for a, b in (gdist.shard_range(m, r, ctx.world) for r in range(ctx.world))]
+    both = torch.stack([mean_l, var_l], dim=0).contiguous()   # (2, U, m_r)
+    allb = gdist.gather_cols(ctx, both, counts)
+    if allb is None:
+        return None
+    return allb[0], allb[1]
 
 
 def unit_order(rank_major: torch.Tensor, n_units: int, world: int) -> torch.Tensor:

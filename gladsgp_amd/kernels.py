@@ -110,14 +110,56 @@ class Cholesky:
         return self.linv_buf.transpose(-1, -2)[:, : self.n, : self.n]
 
     def check(self) -> None:
-        bad = torch.nonzero(self.info).flatten().tolist()
-        if bad:
-            raise ValueError(f"matrix not positive definite (info={self.info[bad].tolist()} for "
-                             f"problems {bad})")
+        check_info(self.info)
 
 
-def cholesky_inverse(G: torch.Tensor, overwrite: bool = True) -> Cholesky:
-    """Blocked MFMA Cholesky A = L L^T with L^-1, logdet and LAPACK info per problem."""
+class FactorizationInternalError(RuntimeError):
+    """info = -1: the persistent factorisation gave up on a bounded wait (an internal error of
+    the library, never a property of the matrix)."""
+
+
+def check_info(info: torch.Tensor) -> None:
+    """Raise for any problem whose factorisation did not succeed: info = -1 is an internal
+    error (:class:`FactorizationInternalError`), info = j > 0 the LAPACK non-positive-definite
+    pivot (ValueError).  Synchronises with the device."""
+    vals = info.cpu()
+    bad = torch.nonzero(vals).flatten().tolist()
+    if not bad:
+        return
+    internal = [b for b in bad if int(vals[b]) < 0]
+    if internal:
+        raise FactorizationInternalError(
+            f"internal factorisation error (info = -1: a bounded wait of the persistent kernel "
+            f"gave up) for problems {internal}; results are invalid")
+    raise ValueError(f"matrix not positive definite (info={vals[bad].tolist()} for "
+                     f"problems {bad})")
+
+
+class Workspace:
+    """Reusable device scratch (grown on demand, never shrunk; 256-B aligned torch storage)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        return self.buf
+
+
+_POTRF_WS = {}
+
+
+def _potrf_ws(device, nbytes: int) -> torch.Tensor:
+    w = _POTRF_WS.setdefault(str(device), Workspace())
+    return w.get(nbytes, device)
+
+
+def cholesky_inverse(G: torch.Tensor, overwrite: bool = True,
+                     workspace: Workspace | None = None) -> Cholesky:
+    """Blocked MFMA Cholesky A = L L^T with L^-1, logdet and LAPACK info per problem
+    (gp_potrf_inv_ws: the factorisation's scratch comes from ``workspace``, by default a
+    per-device one reused across calls on the current stream)."""
     _check_device(G, "G")
     if G.dtype != F64:
         raise TypeError("G must be float64")
@@ -131,21 +173,16 @@ def cholesky_inverse(G: torch.Tensor, overwrite: bool = True) -> Cholesky:
     Linv = torch.empty((batch, npad, npad), dtype=F64, device=G.device)
     info = torch.empty(batch, dtype=torch.int32, device=G.device)
     logdet = torch.empty(batch, dtype=F64, device=G.device)
-    _capi.call("gp_potrf_inv", A.data_ptr(), n, n, n * n, Linv.data_ptr(), npad, npad * npad,
-               batch, info.data_ptr(), logdet.data_ptr(), _stream(G.device))
+    nbytes = int(_capi.lib().gp_potrf_inv_ws_bytes(n, batch))
+    ws = (workspace.get(nbytes, G.device) if workspace is not None
+          else _potrf_ws(G.device, nbytes))
+    _capi.call("gp_potrf_inv_ws", A.data_ptr(), n, n, n * n, Linv.data_ptr(), npad, npad * npad,
+               batch, info.data_ptr(), logdet.data_ptr(), ws.data_ptr(), ws.numel(),
+               _stream(G.device))
     return Cholesky(n, A, Linv, info, logdet)
 
 
-class PredictWorkspace:
-    """Reusable device scratch for :func:`predict` (grown on demand, never shrunk)."""
-
-    def __init__(self):
-        self.buf = None
-
-    def get(self, nbytes: int, device) -> torch.Tensor:
-        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
-            self.buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
-        return self.buf
+PredictWorkspace = Workspace   # scratch of predict / fit_predict / predict_prepare
 
 
 _DEFAULT_WS = PredictWorkspace()
@@ -208,8 +245,22 @@ class LoglikWorkspace:
     def __init__(self, n: int, batch: int, device):
         self.n, self.batch = n, batch
         nbytes = int(_capi.lib().gp_loglik_ws_bytes(n, batch))
-        self.buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        # zero-filled: the library's sticky internal-error word starts clear
+        self.buf = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
         self.info = torch.zeros(batch, dtype=torch.int32, device=device)
+
+    def check_status(self, reset: bool = True) -> None:
+        """Raise :class:`FactorizationInternalError` if any :func:`loglik` on this workspace
+        since the last check had an internal factorisation error (gp_loglik_status; syncs the
+        current stream).  A non-positive-definite proposal is not an error (ll = -inf)."""
+        rc = _capi.lib().gp_loglik_status(self.buf.data_ptr(), self.n, self.batch,
+                                          1 if reset else 0, _stream(self.buf.device))
+        if rc == _capi.GPFIT_ERR_INTERNAL:
+            raise FactorizationInternalError(
+                "gp_loglik: a factorisation gave up (info = -1) since the last check; the "
+                "chain's likelihood values are invalid")
+        if rc != 0:
+            raise _capi.GPFitError("gp_loglik_status", rc)
 
 
 def loglik(X: torch.Tensor, beta: torch.Tensor, s: torch.Tensor, delta: torch.Tensor,
@@ -339,7 +390,8 @@ def fit_predict(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
     With ``ctx`` the cross-covariance runs on the context's CU-masked stream under the
     factorisation's latency-bound tail, then the per-chunk TRMM + mean/var; without it every
     step runs in order on the current stream.  ``check`` synchronises and raises if a Gram was
-    not positive definite (its mean / var would be unspecified).  Returns (mean, var, chol).
+    not positive definite or its factorisation had an internal error (info = -1): the mean /
+    var would be unspecified.  Returns (mean, var, chol).
     """
     dev = X.device
     X = _as_f64(X, dev, "X")
@@ -393,8 +445,10 @@ def cholesky(G: torch.Tensor, overwrite: bool = True):
     A = G if (overwrite and G.is_contiguous()) else G.contiguous().clone()
     info = torch.empty(batch, dtype=torch.int32, device=G.device)
     logdet = torch.empty(batch, dtype=F64, device=G.device)
-    _capi.call("gp_potrf", A.data_ptr(), n, n, n * n, batch, info.data_ptr(), logdet.data_ptr(),
-               _stream(G.device))
+    nbytes = int(_capi.lib().gp_potrf_ws_bytes(n, batch))
+    ws = _potrf_ws(G.device, nbytes)
+    _capi.call("gp_potrf_ws", A.data_ptr(), n, n, n * n, batch, info.data_ptr(),
+               logdet.data_ptr(), ws.data_ptr(), ws.numel(), _stream(G.device))
     return torch.tril(A.transpose(-1, -2)), info, logdet
 
 

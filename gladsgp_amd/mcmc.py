@@ -369,6 +369,9 @@ class GPUSampler:
                     rec["lamWs"][i].copy_(st.lamWs)
                     rec["lamWOs"][i].copy_(st.lamWOs)
                     rec["logPost"][i].copy_(self.lp)
+        # one host check per run: a factorisation that gave up (info = -1) would otherwise be a
+        # silently rejected proposal (ll = NaN); a non-PD proposal (ll = -inf) is a rejection
+        self.ws.check_status()
         return {k: v.cpu().numpy() for k, v in rec.items()} if record else None
 
 

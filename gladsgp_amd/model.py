@@ -56,9 +56,15 @@ def init_model(t_std, y_sim, exp, p, data_dir="data/", sd_threshold=1e-6, recomp
     if recompute or not have:
         r = min(PMAX, *sd_.y_std.shape)
         U, S, Vh = randomized_svd(sd_.y_std, r, k=0, q=1, omega=omega)
-        np.save(pca_fpattern.format(exp, "U"), U[:, :PMAX].cpu().numpy())
-        np.save(pca_fpattern.format(exp, "S"), S.cpu().numpy())
-        np.save(pca_fpattern.format(exp, "Vh"), Vh[:PMAX, :].cpu().numpy())
+        # the reference's y_std has y_sim's dtype (float32 in fit_models / load_model), and its
+        # randomized_svd returns (and init_model caches) that dtype (src/svd.py:51-68,
+        # model.py:87-89); the build computes in fp64 and casts the cached arrays alike
+        ydt = y_sim.dtype if torch.is_tensor(y_sim) else np.asarray(y_sim).dtype
+        f32 = ydt in (np.float32, torch.float32)
+        cast = (lambda a: a.to(torch.float32)) if f32 else (lambda a: a)  # noqa: E731
+        np.save(pca_fpattern.format(exp, "U"), cast(U[:, :PMAX]).cpu().numpy())
+        np.save(pca_fpattern.format(exp, "S"), cast(S).cpu().numpy())
+        np.save(pca_fpattern.format(exp, "Vh"), cast(Vh[:PMAX, :]).cpu().numpy())
     # always use the saved matrices (model.py:91-94)
     S = np.load(pca_fpattern.format(exp, "S"))
     Vh = np.load(pca_fpattern.format(exp, "Vh"))

@@ -1,0 +1,307 @@
+"""Test-point sharding of single-output GPs across ranks ("single-output GP").
+
+The reference's scalar consumers predict one GP (P = 1) per model at many test points:
+``fit_scalar_models.py:477-481`` (64 posterior samples), ``mean_response.py:114-126``
+(16 samples), and the BASELINE C2/C3 configurations (one GP, m = 10k / 100k).  Their units
+(sample, PC) are too few to deal across 8 GPUs, so here the m test points are split instead:
+rank r predicts the contiguous block ``shard_range`` of the points and one gather brings the
+(mean, var) blocks to rank 0.
+
+Two ways to get every rank the factor it needs:
+
+* ``mode="redundant"``: every rank builds the Gram and factorises it itself (gp_fit_predict
+  on its block; the Amdahl term is the factorisation, ~2 ms of a 27 ms C3 step);
+* ``mode="broadcast"``: rank 0 alone factorises and broadcasts L^-1 (its lower triangle packed,
+  half the bytes of the padded square) while its own block is shortened by the factorisation's
+  time in test-point equivalents (``split_counts``), so all ranks finish together.
+
+:class:`PipelinedPredictor` runs a *stream* of GPs as a two-stage pipeline: in step k rank 0
+factorises GP k+1 and broadcasts its L^-1 (asynchronously over RCCL, double-buffered) while
+every rank predicts GP k on its block; each step ends with one gather to rank 0.  A GP's
+latency is two steps; the throughput is what the 1->8 GPU scaling bench reports.
+
+SPMD convention: every rank passes the same hyperparameters and design (as torch DDP code
+does); only rank 0's factorisation is used in the broadcast modes.  All arithmetic is in
+libgpfit (gp_gram_ardse, gp_potrf_inv_ws, gp_predict, gp_fit_predict); collectives are
+torch.distributed (RCCL over xGMI on GPUs, gloo on the CPU tests).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+from . import _capi, kernels
+from . import dist as gdist
+
+F64 = torch.float64
+
+
+def split_counts(m: int, world: int, rank0_extra_points: float = 0.0) -> list[int]:
+    """Test points per rank: rank 0 takes ``rank0_extra_points`` fewer than an even share (the
+    factorisation it runs in addition, in test-point equivalents), the others split the rest
+    evenly (balanced to within one point)."""
+    if world <= 1:
+        return [m]
+    m1 = int(np.ceil((m + rank0_extra_points) / world))
+    m0 = max(0, m - (world - 1) * m1)
+    rest = [b - a for a, b in (gdist.shard_range(m - m0, r, world - 1) for r in range(world - 1))]
+    return [m0] + rest
+
+
+def _offsets(counts: list[int]) -> list[int]:
+    return [int(x) for x in np.concatenate([[0], np.cumsum(counts)[:-1]])]
+
+
+class LinvPacker:
+    """L^-1's nonzero part (column c of the column-major buffer from row c on) as one flat
+    vector: what the broadcast carries (about half the padded square)."""
+
+    def __init__(self, npad: int, device):
+        tri = torch.triu_indices(npad, npad, device=device)   # (c, r), r >= c of the [c][r] view
+        self.flat = tri[0] * npad + tri[1]
+        self.numel = int(self.flat.numel())
+
+    def pack(self, linv_buf: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        return torch.index_select(linv_buf.reshape(-1), 0, self.flat, out=out)
+
+    def unpack(self, packed: torch.Tensor, linv_buf: torch.Tensor) -> torch.Tensor:
+        """Scatter into a buffer whose upper triangle and padding are already zero."""
+        linv_buf.view(-1).index_copy_(0, self.flat, packed)
+        return linv_buf
+
+
+def _wire_bcast(ctx: gdist.Context, t: torch.Tensor, async_op: bool):
+    """Broadcast from rank 0: RCCL moves device tensors in place (optionally async); gloo (CPU
+    tests, several ranks on one GPU) stages through the host, synchronously."""
+    if ctx.backend == "nccl":
+        return tdist.broadcast(t, src=0, async_op=async_op)
+    gdist.broadcast_(ctx, t)
+    return None
+
+
+def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta, s, delta,
+                    s_pred, w, *, mode: str = "redundant", counts: list[int] | None = None,
+                    m_chunk: int = 0, fctx: kernels.FitPredictContext | None = None,
+                    workspace: kernels.Workspace | None = None, gather: bool = True,
+                    check: bool = True):
+    """Posterior mean / variance of one GP at ``Xs`` (m x d, the whole set on every rank),
+    the test points split over ranks.
+
+    Returns ``(mean, var)`` of shape (m,) on rank 0 and ``None`` on the others with
+    ``gather``; else this rank's block ``(mean_r, var_r, (lo, hi))``.  ``counts`` overrides the
+    per-rank split (default: even for "redundant", rank 0 shortened by a measured
+    factorisation time for "broadcast" -- pass :func:`split_counts` of your own calibration to
+    avoid the measurement).  ``check`` synchronises once and raises if the factorisation
+    failed (info != 0); without it the caller owns that check.  Single process: the whole m on
+    this device.
+    """
+    if mode not in ("redundant", "broadcast"):
+        raise ValueError(f"mode must be 'redundant' or 'broadcast', got {mode!r}")
+    dev = X.device
+    world = ctx.world if ctx is not None and ctx.distributed else 1
+    rank = ctx.rank if world > 1 else 0
+    m = Xs.shape[0]
+    n = X.shape[0]
+    if counts is None:
+        if mode == "broadcast" and world > 1:
+            t_fact, t_point = calibrate(ctx, X, Xs, beta, s, delta, s_pred, w)
+            counts = split_counts(m, world, t_fact / t_point)
+        else:
+            counts = [b - a for a, b in (gdist.shard_range(m, r, world) for r in range(world))]
+    if len(counts) != world or sum(counts) != m:
+        raise ValueError(f"counts {counts} do not split m = {m} over {world} ranks")
+    lo = _offsets(counts)[rank]
+    hi = lo + counts[rank]
+    Xl = Xs[lo:hi].contiguous()
+    buf = torch.empty((2, max(hi - lo, 1)), dtype=F64, device=dev)
+    if mode == "redundant" or world == 1:
+        if hi > lo:
+            kernels.fit_predict(X, Xl, beta, s, delta, s_pred, w, m_chunk=m_chunk,
+                                workspace=workspace, out=(buf[0:1, : hi - lo],
+                                                          buf[1:2, : hi - lo]),
+                                ctx=fctx, check=check)
+    else:
+        npad = kernels.padded_n(n)
+        linv = torch.zeros((1, npad, npad), dtype=F64, device=dev)
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+        logdet = torch.zeros(1, dtype=F64, device=dev)
+        packer = LinvPacker(npad, dev)
+        packed = torch.empty(packer.numel, dtype=F64, device=dev)
+        if rank == 0:
+            G = kernels.gram(X, beta, s, delta)
+            ch = kernels.cholesky_inverse(G)
+            if check:
+                ch.check()
+            packer.pack(ch.linv_buf, packed)
+        _wire_bcast(ctx, packed, async_op=False)
+        if rank != 0:
+            packer.unpack(packed, linv)
+            ch = kernels.Cholesky(n, None, linv, info, logdet)
+        if hi > lo:
+            kernels.predict(ch, X, Xl, beta, s, s_pred, w, m_chunk=m_chunk, workspace=workspace,
+                            out=(buf[0:1, : hi - lo], buf[1:2, : hi - lo]))
+    mine = buf[:, : hi - lo]
+    if not gather:
+        return mine[0], mine[1], (lo, hi)
+    if world == 1:
+        return mine[0], mine[1]
+    res = gdist.gather_cols(ctx, mine.contiguous(), counts)
+    if res is None:
+        return None
+    return res[0], res[1]
+
+
+def calibrate(ctx: gdist.Context, X, Xs, beta, s, delta, s_pred, w, points: int = 16384,
+              reps: int = 3) -> tuple[float, float]:
+    """Rank 0 measures one factorisation (Gram + gp_potrf_inv) and the prediction time per test
+    point (median of ``reps``); the pair is broadcast so every rank computes the same split."""
+    dev = X.device
+    calib = torch.zeros(2, dtype=F64, device=dev)
+    if ctx is None or not ctx.distributed or ctx.rank == 0:
+        mc = min(Xs.shape[0], points)
+        Xc = Xs[:mc].contiguous()
+        tf, tp = [], []
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            ch = kernels.cholesky_inverse(kernels.gram(X, beta, s, delta))
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            kernels.predict(ch, X, Xc, beta, s, s_pred, w)
+            torch.cuda.synchronize(dev)
+            tf.append(t1 - t0)
+            tp.append((time.perf_counter() - t1) / mc)
+        calib[0], calib[1] = sorted(tf)[reps // 2], sorted(tp)[reps // 2]
+    if ctx is not None and ctx.distributed:
+        gdist.broadcast_(ctx, calib)
+    return float(calib[0]), float(calib[1])
+
+
+class PipelinedPredictor:
+    """A stream of single-output GPs over shared (X, Xs), test points split over ranks, as a
+    two-stage pipeline: ``step(params_next)`` has rank 0 factorise the next GP and broadcast its
+    L^-1 (async over RCCL, into the other buffer of a double-buffered pair) while every rank
+    predicts the current GP on its block; the (mean, var) blocks are gathered to rank 0.
+
+    Usage::
+
+        pp = PipelinedPredictor(ctx, X, Xs, w, counts=None)     # calibrates the split
+        pp.start(gp0)                 # gp = (beta, s, delta, s_pred): factorise + broadcast GP 0
+        for k in range(K):
+            res_k = pp.step(gp_{k+1})  # predicts GP k; GP k+1 factorised meanwhile
+        res_last = pp.step(None)      # drains the pipeline
+
+    ``step`` returns GP k's (2, m) (mean, var) on rank 0 and None elsewhere.  ``w`` (n,) is the
+    training output shared by the GPs (a different w per GP: pass it in the gp tuple as a fifth
+    element).
+    """
+
+    def __init__(self, ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, w: torch.Tensor,
+                 counts: list[int] | None = None, calib_gp=None, m_chunk: int = 0):
+        self.ctx = ctx
+        self.dev = X.device
+        self.X = X.contiguous()
+        self.n = X.shape[0]
+        self.m = Xs.shape[0]
+        self.w = w.reshape(1, self.n).contiguous()
+        self.m_chunk = m_chunk
+        world = ctx.world if ctx.distributed else 1
+        self.world, self.rank = world, (ctx.rank if ctx.distributed else 0)
+        self.t_fact = self.t_point = None
+        if counts is None:
+            if world > 1:
+                if calib_gp is None:
+                    raise ValueError("PipelinedPredictor: give counts or a calib_gp")
+                b, s_, d_, sp = calib_gp[:4]
+                t_fact, t_point = calibrate(ctx, self.X, Xs, b, s_, d_, sp, self.w)
+                self.t_fact, self.t_point = t_fact, t_point
+                counts = split_counts(self.m, world, t_fact / t_point)
+            else:
+                counts = [self.m]
+        self.counts = counts
+        lo = _offsets(counts)[self.rank]
+        self.ml = counts[self.rank]
+        self.Xl = Xs[lo:lo + self.ml].contiguous()
+        npad = kernels.padded_n(self.n)
+        self.linv = [torch.zeros((1, npad, npad), dtype=F64, device=self.dev) for _ in range(2)]
+        self.info = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.logdet = torch.zeros(1, dtype=F64, device=self.dev)
+        self.packer = LinvPacker(npad, self.dev)
+        self.packed = [torch.empty(self.packer.numel, dtype=F64, device=self.dev)
+                       for _ in range(2)]
+        self.out = torch.empty((2, max(self.ml, 1)), dtype=F64, device=self.dev)
+        self.ws = kernels.Workspace()
+        self.pws = kernels.Workspace()
+        self.k = 0
+        self.gps = [None, None]
+        self.pending = None
+        self.stream = torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _gp(self, gp):
+        b, s, d, sp = gp[:4]
+        t = lambda a: torch.as_tensor(a, dtype=F64, device=self.dev)  # noqa: E731
+        w = self.w if len(gp) < 5 else t(gp[4]).reshape(1, self.n).contiguous()
+        return (t(b).reshape(1, -1).contiguous(), t(s).reshape(1), t(d).reshape(1),
+                t(sp).reshape(1), w)
+
+    def _factor(self, slot: int) -> None:
+        """Rank 0: GP's Gram -> L, L^-1 into linv[slot] (gp_gram_ardse, gp_potrf_inv_ws)."""
+        b, s, d, _, _ = self.gps[slot]
+        G = kernels.gram(self.X, b, s, d)
+        nbytes = int(_capi.lib().gp_potrf_inv_ws_bytes(self.n, 1))
+        ws = self.pws.get(nbytes, self.dev)
+        npad = self.linv[slot].shape[1]
+        _capi.call("gp_potrf_inv_ws", G.data_ptr(), self.n, self.n, self.n * self.n,
+                   self.linv[slot].data_ptr(), npad, npad * npad, 1, self.info.data_ptr(),
+                   self.logdet.data_ptr(), ws.data_ptr(), ws.numel(), self.stream)
+
+    def _bcast(self, slot: int):
+        if self.rank == 0:
+            self.packer.pack(self.linv[slot], self.packed[slot])
+        if self.world == 1:
+            return None
+        return _wire_bcast(self.ctx, self.packed[slot], async_op=True)
+
+    def start(self, gp) -> None:
+        """Factorise and broadcast the first GP (the pipeline's prologue)."""
+        self.k = 0
+        self.gps[0] = self._gp(gp)
+        if self.rank == 0:
+            self._factor(0)
+        self.pending = self._bcast(0)
+
+    def step(self, gp_next):
+        """Predict GP k (broadcast earlier) on this rank's block while rank 0 factorises and
+        broadcasts ``gp_next`` (None: nothing more to factorise); gather GP k's blocks."""
+        k = self.k
+        cur, nxt = k % 2, (k + 1) % 2
+        nxt_req = None
+        if gp_next is not None:
+            self.gps[nxt] = self._gp(gp_next)
+            if self.rank == 0:
+                self._factor(nxt)
+            nxt_req = self._bcast(nxt)
+        if self.pending is not None:
+            self.pending.wait()
+        if self.rank != 0 and self.world > 1:
+            self.packer.unpack(self.packed[cur], self.linv[cur])
+        b, s, _, sp, w = self.gps[cur]
+        ch = kernels.Cholesky(self.n, None, self.linv[cur], self.info, self.logdet)
+        if self.ml:
+            kernels.predict(ch, self.X, self.Xl, b, s, sp, w, m_chunk=self.m_chunk,
+                            workspace=self.ws, out=(self.out[0:1, : self.ml],
+                                                    self.out[1:2, : self.ml]))
+        res = gdist.gather_cols(self.ctx, self.out[:, : self.ml], self.counts) \
+            if self.world > 1 else self.out[:, : self.ml]
+        self.pending = nxt_req
+        self.k = k + 1
+        return res
+
+    def finish(self) -> None:
+        """Wait for an outstanding broadcast (after the last ``step``)."""
+        if self.pending is not None:
+            self.pending.wait()
+            self.pending = None

@@ -102,8 +102,11 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
     when ``X`` is numpy, torch device tensors otherwise.  ``omega`` overrides the test matrix;
     by default it is drawn exactly as the reference does (``np.random.normal(size=(n, p+k))``
     cast to float32), so a seeded ``np.random`` reproduces the reference's Omega.
+    Output dtype follows the reference's numpy promotion (src/svd.py:51-68: a float32 X times
+    the float32 Omega stays float32, float64 X gives float64); the arithmetic is fp64 either way.
     """
     as_numpy = not torch.is_tensor(X)
+    f32_out = (np.asarray(X).dtype == np.float32) if as_numpy else (X.dtype == torch.float32)
     dev = _device(device if as_numpy else (device or X.device))
     Xt = torch.as_tensor(np.asarray(X) if as_numpy else X, dtype=torch.float64, device=dev)
     Xt = Xt.contiguous()
@@ -138,6 +141,8 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
     S_t = S[:p].contiguous()
     Vh_t = Vh.logical()[:p, :].contiguous()
     out = (U_t, S_t, Vh_t)
+    if f32_out:
+        out = tuple(t.to(torch.float32) for t in out)
     if as_numpy:
         out = tuple(t.cpu().numpy() for t in out)
     if return_error:

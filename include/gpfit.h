@@ -9,9 +9,12 @@
  *
  * Conventions (all entry points):
  *  - every pointer is caller-owned DEVICE memory.  The library allocates nothing persistent:
- *    workspaces are sized by the *_ws_bytes() functions and passed in; the only library-owned
- *    objects are the streams/events of an explicit gp_ctx (gp_ctx_create / gp_ctx_destroy),
- *    and gp_potrf's stream-ordered D_k scratch (hipMallocAsync / hipFreeAsync in the call);
+ *    workspaces are sized by the *_ws_bytes() functions and passed in (256-byte aligned); the
+ *    only library-owned objects are the streams/events of an explicit gp_ctx (gp_ctx_create /
+ *    gp_ctx_destroy).  The two convenience forms gp_potrf_inv and gp_potrf take no workspace
+ *    and use stream-ordered scratch of gp_potrf_inv_ws_bytes / gp_potrf_ws_bytes bytes instead
+ *    (hipMallocAsync / hipFreeAsync inside the call, freed on every path); their _ws forms and
+ *    every other entry point allocate nothing;
  *  - matrices are column-major with a leading dimension (LAPACK layout), element (i,j) at
  *    A[i + j*ld]; design matrices X (n x d) are row-major with row stride ldx >= d;
  *  - `batch` independent problems share X / Xs; per-problem operands advance by the given
@@ -21,7 +24,9 @@
  *    captured into a hipGraph;
  *  - return 0 on success, -k when argument k is invalid (LAPACK style), or
  *    GPFIT_ERR_HIP - hipError_t for a launch failure.  A non-positive-definite pivot is not an
- *    error return: it is reported per problem in info[b] (LAPACK potrf semantics).
+ *    error return: it is reported per problem in info[b] (LAPACK potrf semantics); info[b] = -1
+ *    reports an internal error of the factorisation (a bounded wait of the persistent kernel
+ *    gave up), never a pivot: the problem's outputs are then unspecified.
  */
 #ifndef GPFIT_H
 #define GPFIT_H
@@ -34,6 +39,7 @@ extern "C" {
 
 #define GPFIT_ERR_HIP (-1000)
 #define GPFIT_ERR_RCCL (-3000)  /* gp_comm_*: GPFIT_ERR_RCCL - ncclResult_t; RCCL not loadable */
+#define GPFIT_ERR_INTERNAL (-2000)  /* a factorisation reported info = -1 (gp_loglik_status) */
 #define GPFIT_MAX_DIM 32      /* largest input dimension d supported by the kernels      */
 #define GPFIT_TILE 128        /* row padding of the L^-1 buffer (predict MFMA tile edge) */
 
@@ -72,12 +78,20 @@ int gp_cross_ardse(const double* X, int n, int ldx, const double* Xs, int m, int
  *   left untouched, as LAPACK dpotrf('L')), Linv_b = L_b^-1 (lower; the upper triangle and the
  *   padding rows/cols n..gp_padded_n(n)-1 are zeroed), logdet[b] = log|A_b| = 2 sum log L_ii,
  *   info[b] = 0, or j (1-based) when the leading minor of order j is not positive definite
- *   (then L_b / Linv_b / logdet[b] are unspecified).
+ *   (then L_b / Linv_b / logdet[b] are unspecified), or -1 for an internal error (above).
  * Linv_b needs ldinv >= gp_padded_n(n) and gp_padded_n(n) columns.  info / logdet may be NULL.
  * Replaces the dense SPD factorisation / solve inside SEPIA's likelihood and prediction
  * (LAPACK potrf/gesv), scipy.linalg.cholesky in examples/01...ipynb:66,144 and GPmodule's
  * K_inv (examples/02...ipynb:232).
+ * gp_potrf_inv_ws is the same with caller-owned scratch `ws` of gp_potrf_inv_ws_bytes(n, batch)
+ * bytes (the persistent factorisation's task list and flags; 0 bytes when n is beyond its
+ * range); gp_potrf_inv allocates that scratch stream-ordered itself.
  */
+long long gp_potrf_inv_ws_bytes(int n, int batch);
+int gp_potrf_inv_ws(double* A, int n, int lda, long long strideA,
+                    double* Linv, int ldinv, long long strideInv,
+                    int batch, int* info, double* logdet, void* ws, long long ws_bytes,
+                    hipStream_t stream);
 int gp_potrf_inv(double* A, int n, int lda, long long strideA,
                  double* Linv, int ldinv, long long strideInv,
                  int batch, int* info, double* logdet, hipStream_t stream);
@@ -88,8 +102,13 @@ int gp_potrf_inv(double* A, int n, int lda, long long strideA,
  * 1-based order of the first non-positive-definite leading minor.  Same sweep and arithmetic as
  * gp_potrf_inv without the inverse (L is bit-identical to gp_potrf_inv's).  info / logdet may
  * be NULL.  Replaces the factorisation SURVEY §8b names gp_potrf (LAPACK potrf inside SEPIA's
- * likelihood, scipy.linalg.cholesky in examples/01...ipynb:66,144).
+ * likelihood, scipy.linalg.cholesky in examples/01...ipynb:66,144).  gp_potrf_ws takes the
+ * scratch (the D_k = L_kk^-1 blocks and the persistent kernel's task list / flags) from the
+ * caller: gp_potrf_ws_bytes(n, batch) bytes.
  */
+long long gp_potrf_ws_bytes(int n, int batch);
+int gp_potrf_ws(double* A, int n, int lda, long long strideA, int batch, int* info,
+                double* logdet, void* ws, long long ws_bytes, hipStream_t stream);
 int gp_potrf(double* A, int n, int lda, long long strideA, int batch, int* info,
              double* logdet, hipStream_t stream);
 
@@ -195,8 +214,9 @@ int gp_ctx_destroy(void* ctx);
  * CU-masked, beside the factorisation | once the factorisation is done z = L^-1 w, then per
  * chunk, once that chunk's cross-covariance is done, its TRMM, and one mean/var pass) and joins
  * back: the caller sees one stream-ordered operation.  `ws` holds
- * gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes.  The prediction runs whatever info
- * says: mean / var of a problem with info[b] != 0 are unspecified (check info).
+ * gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes (the factorisation's scratch included).
+ * The prediction runs whatever info says: mean / var of a problem with info[b] != 0 are
+ * unspecified (check info; -1 is an internal error, see the conventions).
  * Replaces the reference's fit-then-predict sequence per GP (SEPIA likelihood factorisation +
  * SepiaEmulatorPrediction, time_predictions.py:76-79) at the bench configuration.
  */
@@ -211,9 +231,14 @@ int gp_fit_predict(const double* X, int ldx, const double* Xs, int ldxs, int n, 
 /*
  * Batched GP log-likelihood in one stream-ordered call: Gram (gp_gram_ardse) -> Cholesky
  * (gp_potrf_inv) -> ll[b] = -(1/2 ||L_b^-1 w_b||^2 + 1/2 log|G_b|), no 2*pi term, with
- * ll[b] = -inf where the factorisation failed (info[b] != 0, optionally copied out to `info`).
- * `ws` is caller-owned device scratch of gp_loglik_ws_bytes(n, batch) bytes.  Never syncs,
- * so a Metropolis sweep can be stream-ordered (and graph-captured) end to end.
+ * ll[b] = -inf where G_b is not positive definite (info[b] > 0: a proposal the sampler rejects)
+ * and ll[b] = NaN where the factorisation gave up (info[b] = -1), which also raises a sticky
+ * status word in `ws` (info optionally copied out to `info`).  `ws` is caller-owned device
+ * scratch of gp_loglik_ws_bytes(n, batch) bytes, zero-filled before its first use.  Never
+ * syncs, so a Metropolis sweep can be stream-ordered (and graph-captured) end to end;
+ * gp_loglik_status reads the status word afterwards (it synchronises `stream`): 0, or
+ * GPFIT_ERR_INTERNAL when any gp_loglik on this workspace since the last reset had an internal
+ * factorisation error; `reset` clears the word.
  * Replaces the per-PC term of SEPIA's logLik evaluated by SepiaModel.do_mcmc /
  * tune_step_sizes (src/model.py:234-235): Sigma_j = s_j R(beta_j) + delta_j I, w = w_hat_j.
  */
@@ -221,6 +246,7 @@ long long gp_loglik_ws_bytes(int n, int batch);
 int gp_loglik(const double* X, int n, int d, int ldx, const double* beta, int ldbeta,
               const double* s, const double* delta, const double* w, int ldw, int batch,
               void* ws, long long ws_bytes, double* ll, int* info, hipStream_t stream);
+int gp_loglik_status(void* ws, int n, int batch, int reset, hipStream_t stream);
 
 /*
  * One marginal realisation per entry: out[i] = mean[i] + sqrt(max(var[i], 0)) z_i, z_i ~ N(0,1)
@@ -311,6 +337,14 @@ int gp_gather(void* comm, const void* send, long long bytes, void* recv, int roo
 int gp_profile_enable(int capacity);
 int gp_profile_reset(void);
 int gp_profile_read(int id, int* count, double* total_ms, double* max_ms);
+
+/* Test / diagnostics hook, process-wide (the library's one mutable setting): the number of
+ * polls a wait of the persistent factorisation makes before it gives up and reports info = -1
+ * for the launches enqueued afterwards.  polls > 0 sets it, 0 restores the default (2^22, far
+ * beyond any legitimate wait), < 0 makes every later factorisation start with its problems
+ * given up (info = -1 deterministically: the tests of the internal-error path).  Returns the
+ * previous setting. */
+long long gp_set_poll_budget(long long polls);
 
 #ifdef __cplusplus
 }

@@ -17,26 +17,3 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
-
-
-if os.environ.get("GPFIT_PP_WATCHDOG"):   # debug only: report a stuck persistent factorisation
-    import threading
-    import time
-
-    import torch
-
-    _PP_DBG = torch.full((4 * 256,), -1, dtype=torch.int32).pin_memory()
-    os.environ["GPFIT_PP_DEBUG_PTR"] = str(_PP_DBG.data_ptr())
-    _PP_LAST = {"t": time.time(), "snap": None}
-
-    def _pp_watch():
-        while True:
-            time.sleep(5)
-            snap = _PP_DBG.numpy().reshape(-1, 4)[:, :3].copy()
-            if _PP_LAST["snap"] is not None and (snap == _PP_LAST["snap"]).all() and \
-                    (snap[:, 1] != 99).any() and (snap[:, 0] >= 0).any():
-                act = [(i, *snap[i]) for i in range(len(snap)) if snap[i][0] >= 0]
-                print("PP WATCHDOG (wg, task, code, val):", act, flush=True)
-            _PP_LAST["snap"] = snap
-
-    threading.Thread(target=_pp_watch, daemon=True).start()

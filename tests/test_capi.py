@@ -87,9 +87,13 @@ def test_argument_validation_returns_lapack_style_codes(lib):
     rc = lib.gp_loglik(dummy, 64, 0, 2, dummy, 2, dummy, dummy, dummy, 64, 1, dummy, 1 << 30,
                        dummy, None, None)
     assert rc == -3   # d < 1
-    rc = lib.gp_loglik(dummy, 64, 2, 2, dummy, 2, dummy, dummy, dummy, 64, 2, dummy, 16,
+    wsp = ctypes.c_void_p(256)                       # workspaces are 256-B aligned
+    rc = lib.gp_loglik(dummy, 64, 2, 2, dummy, 2, dummy, dummy, dummy, 64, 2, wsp, 16,
                        dummy, None, None)
     assert rc == -13  # workspace too small
+    rc = lib.gp_loglik(dummy, 64, 2, 2, dummy, 2, dummy, dummy, dummy, 64, 2, dummy, 1 << 30,
+                       dummy, None, None)
+    assert rc == -12  # workspace not 256-B aligned
     assert lib.gp_loglik(dummy, 0, 2, 2, dummy, 2, dummy, dummy, dummy, 0, 1, None, 0, dummy,
                          None, None) == 0
     # gp_fit_predict: validated before anything is enqueued
@@ -97,7 +101,7 @@ def test_argument_validation_returns_lapack_style_codes(lib):
                                                                                        100000,
                                                                                        1, 0)
     args = [dummy, 2, dummy, 2, 100, 10, 2, dummy, 2, dummy, dummy, dummy, dummy, 100,
-            dummy, 100, 10000, dummy, 128, 128 * 128, None, None, dummy, dummy, 10, 1, dummy,
+            dummy, 100, 10000, dummy, 128, 128 * 128, None, None, dummy, dummy, 10, 1, wsp,
             1 << 40, 0, None, None]
     bad = list(args)
     bad[10] = None                                   # delta
@@ -108,6 +112,9 @@ def test_argument_validation_returns_lapack_style_codes(lib):
     bad = list(args)
     bad[27] = 16                                     # workspace too small
     assert lib.gp_fit_predict(*bad) == -22
+    bad[26] = ctypes.c_void_p(16)                    # workspace not 256-B aligned
+    bad[27] = 1 << 40
+    assert lib.gp_fit_predict(*bad) == -21
 
 
 def test_new_entry_points_validate(lib):
@@ -154,3 +161,28 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(_capi, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(_capi.GPFitUnavailable):
         _capi.lib()
+
+
+def test_factorisation_workspace_entry_points(lib):
+    """gp_potrf_inv_ws / gp_potrf_ws: sized scratch, validated before any launch; the
+    allocating forms validate before allocating."""
+    dummy = ctypes.c_void_p(16)
+    wsp = ctypes.c_void_p(256)
+    inv = lib.gp_potrf_inv_ws_bytes(4096, 1)
+    assert inv > 0 and lib.gp_potrf_inv_ws_bytes(4096, 8) > inv
+    assert lib.gp_potrf_inv_ws_bytes(-1, 1) == -1
+    assert lib.gp_potrf_inv_ws_bytes(64 * 241, 1) == 0          # beyond the persistent kernel
+    assert lib.gp_potrf_ws_bytes(512, 4) > lib.gp_potrf_inv_ws_bytes(512, 4)
+    # gp_fit_predict / gp_loglik carry the factorisation's scratch in their own workspace
+    assert (lib.gp_fit_predict_ws_bytes(4096, 100000, 1, 0) >=
+            lib.gp_predict_prepared_ws_bytes(4096, 100000, 1, 0) + inv)
+    assert lib.gp_loglik_ws_bytes(512, 8) > lib.gp_potrf_inv_ws_bytes(512, 8)
+    assert lib.gp_potrf_inv_ws(None, 10, 10, 100, dummy, 128, 128 * 128, 1, None, None, wsp,
+                               1 << 30, None) == -1
+    assert lib.gp_potrf_inv_ws(dummy, 100, 100, 10000, dummy, 64, 4096, 1, None, None, wsp,
+                               1 << 30, None) == -6
+    assert lib.gp_potrf_ws(dummy, 4, 3, 16, 1, None, None, wsp, 1 << 30, None) == -3
+    assert lib.gp_potrf_ws(dummy, 0, 1, 0, 1, None, None, None, 0, None) == 0
+    assert lib.gp_potrf(dummy, 4, 4, 8, 2, None, None, None) == -4   # before any allocation
+    assert lib.gp_loglik_status(None, 4, 1, 0, None) == -1
+    assert lib.gp_loglik_status(wsp, 0, 1, 0, None) == 0

@@ -102,3 +102,89 @@ def test_gloo_world2_broadcast_gather_max():
         ok_b, ok_g, t, ok_s, ok_a, ok_y = results[r]
         assert ok_b and ok_g and ok_s and ok_a and ok_y
         assert t == 2.0
+
+
+def test_split_counts():
+    from gladsgp_amd.sharded import split_counts
+    assert split_counts(100, 1, 40.0) == [100]
+    for m, world, extra in ((100000, 8, 9200.0), (40000, 2, 3000.0), (10, 4, 0.0),
+                            (7, 8, 0.0), (100, 3, 1e9)):
+        c = split_counts(m, world, extra)
+        assert len(c) == world and sum(c) == m and min(c) >= 0
+        assert max(c[1:]) - min(c[1:]) <= 1
+        assert c[0] <= max(c[1:])
+    # rank 0's share is shortened by the extra work in points (C3 at 8 GPUs: ~9.2k points)
+    c = split_counts(100000, 8, 9200.0)
+    assert abs((c[0] + 9200.0) - c[1]) <= 8
+
+
+def _points_worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from gladsgp_amd import dist as gdist
+    from gladsgp_amd.emulator import assemble_points
+    from gladsgp_amd.sharded import LinvPacker
+    ctx = gdist.init_from_env("cpu")
+    try:
+        # test-point sharding of U units (EmulatorPrediction shard="points"): every rank holds
+        # all units on its block of the m points; rank 0 reassembles (U, m)
+        U, m = 3, 11
+        lo, hi = gdist.shard_range(m, rank, world)
+        j = torch.arange(lo, hi, dtype=torch.float64)
+        mean_l = torch.stack([100.0 * u + j for u in range(U)])
+        out = assemble_points(ctx, mean_l, -mean_l, m)
+        if rank == 0:
+            ref = torch.stack([100.0 * u + torch.arange(m, dtype=torch.float64)
+                               for u in range(U)])
+            ok_p = bool(torch.equal(out[0], ref) and torch.equal(out[1], -ref))
+        else:
+            ok_p = out is None
+        # L^-1 broadcast packed to its lower triangle (sharded.LinvPacker), rebuilt exactly
+        npad = 8
+        full = torch.tril(torch.arange(1.0, npad * npad + 1, dtype=torch.float64)
+                          .reshape(npad, npad)).T.contiguous().reshape(1, npad, npad)
+        pk = LinvPacker(npad, torch.device("cpu"))
+        packed = torch.empty(pk.numel, dtype=torch.float64)
+        if rank == 0:
+            pk.pack(full, packed)
+        gdist.broadcast_(ctx, packed)
+        got = pk.unpack(packed, torch.zeros((1, npad, npad), dtype=torch.float64))
+        ok_l = bool(torch.equal(got, full)) and pk.numel == npad * (npad + 1) // 2
+        results[rank] = (ok_p, ok_l)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_point_shards_and_packed_linv():
+    world = 2
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_points_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+    for r in range(world):
+        assert results[r] == (True, True), results[r]
+
+
+@pytest.mark.timeout(240)
+def test_bench_gpus_flag_launches_ranks():
+    """``python bench.py --gpus 2`` with no launcher starts two ranks itself (a child
+    torch.distributed.run; --dry-run: gloo on the host, no GPU work) and rank 0's JSON reports
+    n_gpus = 2; a process group smaller than --gpus is refused (non-zero exit)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--dry-run"], capture_output=True, text=True, env=env, timeout=200)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] is True
+    env1 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--dry-run"], capture_output=True, text=True, env=env1, timeout=200)
+    assert r.returncode != 0 and "2 but 1 ranks" in r.stderr

@@ -7,7 +7,9 @@ paths of SURVEY §8e end to end, each rank computing on cuda:0.
 * field reconstruction: get_y(ctx=...) splits K by output columns after broadcasting w;
   gathered, it equals the unsharded get_y, and each rank's block (gather=False) its columns;
 * strong-scaled single-output GP (bench C3): rank r predicts shard_range(m, r, 2) with
-  gp_fit_predict and gather_cols reassembles (2, m) — bit-identical to one rank doing all m.
+  gp_fit_predict and gather_cols reassembles (2, m) — bit-identical to one rank doing all m;
+* gladsgp_amd.sharded: the two-stage pipeline over a stream of GPs and predict_sharded in
+  both factorisation modes; EmulatorPrediction's test-point sharding of scalar GPs.
 """
 import os
 import socket
@@ -122,40 +124,76 @@ def _pipe_worker(rank, world, port, results):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import sys
-    import time
-    import types
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
-    import bench
     from gladsgp_amd import dist as gdist
+    from gladsgp_amd import kernels
+    from gladsgp_amd.sharded import PipelinedPredictor, predict_sharded, split_counts
     ctx = gdist.init_from_env("cuda", backend="gloo", device_index=0)
+    out = {}
     try:
-        X, y, beta, Xs, s, delta = bench.c3_inputs(640, 40000, 8)
-        args = types.SimpleNamespace(warmup=2, steps=3, m_chunk=0)
-
-        def timed(fn, steps):
-            gdist.barrier(ctx)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                fn()
-            torch.cuda.synchronize()
-            gdist.barrier(ctx)
-            return gdist.max_over_ranks(ctx, time.perf_counter() - t0)
-
-        pipe = bench.c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed)
-        results[rank] = {"counts": pipe["counts"], "check": pipe["check"]}
-    except Exception as exc:  # noqa: BLE001 - reported to the parent
+        dev = ctx.device
+        n, m, d = 640, 40000, 8
+        X = np.random.default_rng(0).random((n, d))
+        a = np.random.default_rng(1).uniform(0, 1, d)
+        y = np.sin(2 * np.pi * X @ a) + 0.1 * np.sum(X * X, axis=1)
+        beta = np.random.default_rng(3).uniform(0.5, 5.0, d)
+        Xs = np.random.default_rng(2).random((m, d))
+        T = lambda v: torch.as_tensor(np.ascontiguousarray(v), device=dev)  # noqa: E731
+        Xd, Xsd, yd = T(X), T(Xs), T(y).reshape(1, n)
+        sd = torch.tensor([1.0], dtype=torch.float64, device=dev)
+        dd = torch.tensor([1e-6], dtype=torch.float64, device=dev)
+        betas = [T(beta * (1.0 + 1e-3 * k)).reshape(1, d) for k in range(5)]
+        gps = [(b, sd, dd, sd) for b in betas]
+        # the package's two-stage pipeline over 5 GPs: GP k predicted while k+1 is factorised
+        pp = PipelinedPredictor(ctx, Xd, Xsd, yd, calib_gp=gps[0])
+        pp.start(gps[0])
+        res = [pp.step(gps[k + 1] if k + 1 < 5 else None) for k in range(5)]
+        pp.finish()
+        out["counts"] = pp.counts
+        # one direct single-rank computation per GP on rank 0, bit-identical to the pipeline
+        # (the same kernels on the same inputs; L^-1 travels packed, unpacked exactly)
+        ok_pipe = True
+        if rank == 0:
+            for k in range(5):
+                ch = kernels.cholesky_inverse(kernels.gram(Xd, betas[k], sd, dd))
+                ch.check()
+                mu, var = kernels.predict(ch, Xd, Xsd, betas[k], sd, sd, yd)
+                ok_pipe &= bool(torch.equal(res[k][0], mu[0]) and torch.equal(res[k][1], var[0]))
+        else:
+            ok_pipe = all(r is None for r in res)
+        out["pipe"] = ok_pipe
+        # predict_sharded, both modes, vs one rank doing all m
+        full = None
+        if rank == 0:
+            ch = kernels.cholesky_inverse(kernels.gram(Xd, betas[2], sd, dd))
+            full = kernels.predict(ch, Xd, Xsd, betas[2], sd, sd, yd)
+        ok_modes = {}
+        for mode, counts in (("redundant", None), ("broadcast", split_counts(m, world, 3000.0)),
+                             ("broadcast", None)):
+            r = predict_sharded(ctx, Xd, Xsd, betas[2], sd, dd, sd, yd, mode=mode, counts=counts)
+            key = f"{mode}-{'given' if counts else 'auto'}"
+            if rank == 0:
+                tol_m = 1e-12 * max(1.0, float(full[0].abs().max()))
+                ok_modes[key] = bool((r[0] - full[0][0]).abs().max() <= tol_m and
+                                     (r[1] - full[1][0]).abs().max() <= 1e-12)
+            else:
+                ok_modes[key] = r is None
+        out["modes"] = ok_modes
+        torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001 - reported to the parent
         import traceback
-        results[rank] = {"error": traceback.format_exc()}
+        out["error"] = traceback.format_exc()
     finally:
+        results[rank] = out
         dist.destroy_process_group()
 
 
-def test_two_ranks_pipelined_c3():
-    """bench.py's N > 1 schedule: rank 0 factorises GP k+1 and broadcasts L^-1 while both ranks
-    predict GP k on their blocks (consecutive GPs differ); the function itself checks the last
-    step's gathered (mean, var) against a direct single-rank computation of that GP."""
+def test_two_ranks_pipelined_and_sharded_single_gp():
+    """gladsgp_amd.sharded (SURVEY §8e single-output GP) with two ranks on the one GPU:
+    PipelinedPredictor (rank 0 factorises GP k+1 and broadcasts L^-1 while both ranks predict
+    GP k on their blocks; consecutive GPs differ) equals a direct computation of every GP bit
+    for bit, and predict_sharded matches one rank doing all m in both factorisation modes."""
     world = 2
     mgr = mp.Manager()
     results = mgr.dict()
@@ -163,7 +201,57 @@ def test_two_ranks_pipelined_c3():
     for r in range(world):
         res = dict(results[r])
         assert "error" not in res, res.get("error")
+        assert res["pipe"], res
+        assert all(res["modes"].values()), res["modes"]
     counts = results[0]["counts"]
     assert sum(counts) == 40000 and len(counts) == 2 and 0 < counts[0] <= counts[1]
-    chk = results[0]["check"]
-    assert chk["gp"] == 4 and chk["max_abs_dmean"] <= 1e-12 and chk["max_abs_dvar"] <= 1e-12, chk
+
+
+def _scalar_worker(rank, world, port, results, tmpdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from gladsgp_amd import dist as gdist
+    from gladsgp_amd import model as gm
+    from gladsgp_amd.emulator import EmulatorPrediction
+    ctx = gdist.init_from_env("cuda", backend="gloo", device_index=0)
+    out = {}
+    try:
+        dev = ctx.device
+        t, y = _ensemble(n=60, ny=300, d=4, seed=3)
+        np.random.seed(0)
+        data, model = gm.init_model(t, y, "sc", 1, data_dir=os.path.join(tmpdir, str(rank)),
+                                    device=dev, verbose=False)
+        rng = np.random.default_rng(4)
+        samples = {"betaU": rng.uniform(0.2, 3.0, (1, 5)), "lamUz": rng.uniform(0.5, 3, (1, 1)),
+                   "lamWs": rng.uniform(200, 3000, (1, 1)), "lamWOs": rng.uniform(50, 500, (1, 1))}
+        t_pred = np.random.default_rng(5).random((1001, 4))
+        # one unit (a scalar GP, one sample) < two ranks: the points are split
+        sh = EmulatorPrediction(model=model, samples=samples, t_pred=t_pred, ctx=ctx)
+        out["shard"] = sh.shard
+        full = EmulatorPrediction(model=model, samples=samples, t_pred=t_pred)
+        if rank == 0:
+            out["eq"] = bool(np.array_equal(sh.w, full.w) and np.array_equal(sh.var, full.var))
+        else:
+            out["eq"] = sh.w is None
+    except Exception:  # noqa: BLE001
+        import traceback
+        out["error"] = traceback.format_exc()
+    finally:
+        results[rank] = out
+        dist.destroy_process_group()
+
+
+def test_two_ranks_scalar_gp_points_sharded(tmp_path):
+    """EmulatorPrediction(ctx=) with fewer (sample, PC) units than ranks (the reference's scalar
+    GPs, fit_scalar_models.py:477-481) shards the test points and equals the unsharded result."""
+    world = 2
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_scalar_worker, args=(world, _free_port(), results, str(tmp_path)), nprocs=world,
+             join=True)
+    for r in range(world):
+        res = dict(results[r])
+        assert "error" not in res, res.get("error")
+        assert res["shard"] == "points" and res["eq"], res

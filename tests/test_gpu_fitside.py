@@ -80,8 +80,16 @@ def test_randomized_svd_vs_reference_golden(dev, golden_dir):
     g = np.load(os.path.join(golden_dir, "svd_ref_64x500.npz"))
     X = g["X"]
     for tag, (p, k) in {"p8": (8, None), "p25k0": (25, 0)}.items():
-        U, S, Vh = randomized_svd(X, p, k=k, q=1, omega=g[f"{tag}_omega"], device=dev)
+        # float32 input -> float32 outputs, as src/svd.py:51-68 returns for a float32 X
+        U32, S32, Vh32 = randomized_svd(X.astype(np.float32), p, k=k, q=1,
+                                        omega=g[f"{tag}_omega"], device=dev)
+        assert U32.dtype == S32.dtype == Vh32.dtype == np.float32
+        U, S, Vh = randomized_svd(X.astype(np.float64), p, k=k, q=1, omega=g[f"{tag}_omega"],
+                                  device=dev)
+        assert U.dtype == np.float64
         assert U.shape == (64, p) and S.shape == (p,) and Vh.shape == (p, 500)
+        np.testing.assert_array_equal(S32, S.astype(np.float32))
+        np.testing.assert_array_equal(U32, U.astype(np.float32))
         # fp64 oracle restatement with the same Omega: tight
         Uo, So, Vo = gp_ref.randomized_svd(X.astype(np.float64), p, k=k, q=1,
                                            omega=g[f"{tag}_omega"])
@@ -127,7 +135,10 @@ def test_randomized_svd_rank_deficient_vs_reference(dev, golden_dir, n):
     g = np.load(os.path.join(golden_dir, "svd_ref_deficient.npz"))
     y_std = g[f"n{n}_y_std"]
     r = min(25, *y_std.shape)
-    U, S, Vh = randomized_svd(y_std, r, k=0, q=1, omega=g[f"n{n}_omega"], device=dev)
+    # fp64 input: fp64 outputs, compared tightly (a float32 input returns float32, as the
+    # reference's src/svd.py does: test_randomized_svd_vs_reference_golden)
+    U, S, Vh = randomized_svd(y_std.astype(np.float64), r, k=0, q=1, omega=g[f"n{n}_omega"],
+                              device=dev)
     assert U.shape == (n, r) and S.shape == (r,) and Vh.shape == (r, y_std.shape[1])
     assert np.all(np.isfinite(U)) and np.all(np.isfinite(S)) and np.all(np.isfinite(Vh))
     np.testing.assert_allclose(U.T @ U, np.eye(r), atol=1e-10)
@@ -183,3 +194,20 @@ def test_randomized_svd_large_rank(dev, p, k):
     tol = 1e-9 * So + 1e-12 * So[0] ** 2 / So
     assert np.all(np.abs(S - So) <= tol)
     np.testing.assert_allclose(U.T @ U, np.eye(p), atol=1e-10)
+
+
+def test_init_model_caches_reference_dtype(dev, tmp_path):
+    """float32 ensembles (fit_models / load_model's default dtype) cache float32
+    pca_*_{U,S,Vh}.npy like the reference (src/svd.py:51, model.py:87-89); float64 stays
+    float64."""
+    from gladsgp_amd import model as gm
+    rng = np.random.default_rng(3)
+    t = rng.random((40, 8))
+    y = 1.0 + np.sin(2 * np.pi * t @ rng.uniform(0, 1, 8))[:, None] * rng.standard_normal(
+        (1, 500)) + 0.05 * rng.standard_normal((40, 500))
+    for dt in (np.float32, np.float64):
+        d = tmp_path / np.dtype(dt).name
+        gm.init_model(t.astype(dt), y.astype(dt), "dt", 4, data_dir=str(d), device=dev,
+                      verbose=False)
+        for a in ("U", "S", "Vh"):
+            assert np.load(d / f"pca_dt_{a}.npy").dtype == dt
