@@ -500,13 +500,11 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
     }
   }
   __syncthreads();
-  // zero the strict upper blocks of L and L^-1
+  // zero the strict upper blocks of L^-1 (the chain's GEMM and the D_j store read the whole
+  // tile; L's upper blocks are never read: it is stored lower-only, then overwritten)
   for (int g = threadIdx.x; g < NB * NB; g += 256) {
     const int r = g >> 6, cc = g & 63;
-    if ((cc >> 4) > (r >> 4)) {
-      T[r * LP + cc] = 0.0;
-      U[r * LP + cc] = 0.0;
-    }
+    if ((cc >> 4) > (r >> 4)) U[r * LP + cc] = 0.0;
   }
   __syncthreads();
   const int f = sm.fail;
@@ -1420,41 +1418,45 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
   double ld_sum = 0.0;
   OpTile tpj;                // P_jj, loaded by the previous step when its partials were ready
   bool pref = false;
+  // L_j,j-1 L_j,j-1^T for step j, computed at the end of step j-1 while that step's stores
+  // drain (zero for j = 0).  Exactly symmetric: element (r, c) and (c, r) sum the same products
+  // in the same order.
+  f64x4 syrk[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) syrk[mi][nj] = zero4();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wr = wv >> 1, wc = wv & 1, li = lane & 15, lk = lane >> 4;
   for (int j = 0; j < N; ++j) {
     const int nb = min(NB, P.n - j * NB);
     PP_MARK(P, 10, j);
     const long long tb0 = (long long)P.ntasks * 6 + ((long long)b * N + j) * 8;
     (void)tb0;
     PP_TRACE(P, tb0 + 0, pp_now());
-    // (a) C_jj = P_jj - L_j,j-1 L_j,j-1^T into As as a full symmetric [row][col] tile.  The
-    // P_jj loads (16-B sc1, the whole tile; only its lower triangle is used) are in flight
-    // during the SYRK.
+    // (a) C_jj = P_jj - syrk into As as a full symmetric [row][col] tile: P_jj's lower triangle
+    // staged in Bs ([col][row]), then every thread writes its own 16 accumulator positions
+    // (mirrored to the lower element of P), identity padding past nb.
     if (!pref) {
       if (j >= 2 && !pp_wait1(F + 2 * N * N + j, abort, P.budget)) return;
       pp_load(tpj, atile(j, j), P.lda, nb, nb);
     }
     PP_TRACE(P, tb0 + 1, pp_now());
-    f64x4 acc[2][2];
-    if (j >= 1) mma64(g_keep, g_keep, acc);
-    else {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = zero4();
-    }
     __syncthreads();
-    acc_to_lds(sm.Bs, acc);                             // Bs[col][row] = acc(row, col)
-    store_op<false>(sm.As, tpj);                        // As[c][r] = P(r, c) (r >= c valid)
+    store_op<false>(sm.Bs, tpj);                        // Bs[c][r] = P(r, c) (r >= c valid)
     __syncthreads();
-    for (int g = threadIdx.x; g < NB * NB; g += 256) {
-      const int r = g & (NB - 1), c = g >> 6;           // lower element (r, c), r >= c
-      if (r < c) continue;
-      double v;
-      if (r < nb) v = sm.As[c * LP + r] - sm.Bs[c * LP + r];
-      else v = (r == c) ? 1.0 : 0.0;
-      sm.As[r * LP + c] = v;
-      sm.As[c * LP + r] = v;
-    }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = wr * 32 + mi * 16 + lk + 4 * q, col = wc * 32 + nj * 16 + li;
+          const int R = row > col ? row : col, C = row > col ? col : row;
+          const double v = R < nb ? sm.Bs[C * LP + R] - syrk[mi][nj][q]
+                                  : (row == col ? 1.0 : 0.0);
+          sm.As[row * LP + col] = v;
+        }
     __syncthreads();
     // (b) factor + invert
     PP_MARK(P, 11, j);
@@ -1471,41 +1473,49 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
     }
     ld_sum += lg;
     PP_MARK(P, 12, j);
-    // L_jj -> A (lower, LAPACK layout), D_j -> X_jj (or the D scratch); sm.As / sm.Bs hold
-    // them as [row][col]
-    {
-      int ldd;
-      double* D = pp_dptr(P, b, j, ldd);
+    int ldd;
+    double* D = pp_dptr(P, b, j, ldd);
+    if (j + 1 >= N) {
+      // last step: D_j -> X_jj (or the D scratch), L_jj -> A (lower, LAPACK layout)
       pp_store_rm(D, ldd, sm.Bs, nb, false);
+      pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);
+      pp_publish(F + j * N + j);
+      PP_TRACE(P, tb0 + 4, pp_now());
+      break;
     }
-    pp_publish(F + j * N + j);
-    pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);   // L_jj: read by nobody in this launch
-    PP_TRACE(P, tb0 + 4, pp_now());
-    if (j + 1 >= N) break;
-    // (c) L_j+1,j = P_j+1,j D_j^T
+    // (c) D_j and L_jj are stored and D_j published right away: LT(j+2, j) -> SP(j+1) -> the
+    // next step's (d) hang on it (publishing D_j after the GEMM instead moved 2-4 us per step
+    // into the chain's wait for SP, profiles/r03/pp_trace_pp1.txt).  The loads of P_j+1,j and
+    // the next P_j+1,j+1 go out with the stores when their partial sums are already published.
     PP_MARK(P, 13, j);
     const int nb1 = min(NB, P.n - (j + 1) * NB);
-    if (j >= 1 && !pp_wait1(F + 2 * N * N + N + j, abort, P.budget)) return;
-    PP_TRACE(P, tb0 + 5, pp_now());
+    pp_store_rm(D, ldd, sm.Bs, nb, false);
+    pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);   // L_jj: read by nobody in this launch
     OpTile tp;
-    pp_load(tp, atile(j + 1, j), P.lda, nb1, NB);      // As[p][r] = P[r][p]
-    // the next step's P_j+1,j+1, in flight under this step's GEMM and stores when its partial
-    // sums are already published
+    const bool spref = j < 1 || pp_test1(F + 2 * N * N + N + j);
+    if (spref) pp_load(tp, atile(j + 1, j), P.lda, nb1, NB);
     pref = j + 1 < 2 || pp_test1(F + 2 * N * N + j + 1);
-    if (pref) {
-      const int nbn = min(NB, P.n - (j + 1) * NB);
-      pp_load(tpj, atile(j + 1, j + 1), P.lda, nbn, nbn);
+    if (pref) pp_load(tpj, atile(j + 1, j + 1), P.lda, nb1, nb1);
+    pp_publish(F + j * N + j);                          // drains stores and loads alike
+    PP_TRACE(P, tb0 + 4, pp_now());
+    if (!spref) {
+      if (!pp_wait1(F + 2 * N * N + N + j, abort, P.budget)) return;
+      pp_load(tp, atile(j + 1, j), P.lda, nb1, NB);    // As[p][r] = P[r][p]
     }
-    __syncthreads();
-    store_op<false>(sm.As, tp);
+    store_op<false>(sm.As, tp);                         // (pp_publish's barrier: As is free)
     __syncthreads();
     PP_MARK(P, 14, j);
-    PP_TRACE(P, tb0 + 6, pp_now());
-    mma64_bt(sm.As, sm.Bs, acc);                       // P D^T, D held [row][col] in Bs
+    PP_TRACE(P, tb0 + 5, pp_now());
+    // (d) L_j+1,j = P_j+1,j D_j^T (D held [row][col] in Bs), kept in LDS for the next SYRK
+    f64x4 acc[2][2];
+    mma64_bt(sm.As, sm.Bs, acc);
     __syncthreads();
     acc_to_lds(g_keep, acc);                           // keep[c][r] = L_j+1,j(r, c)
     __syncthreads();
+    PP_TRACE(P, tb0 + 6, pp_now());
     pp_store_cm(atile(j + 1, j), P.lda, g_keep, nb1, NB, false);
+    // the next step's SYRK runs while L_j+1,j's stores drain, then its flag goes up
+    mma64(g_keep, g_keep, syrk);
     pp_publish(F + (j + 1) * N + j);
     PP_MARK(P, 15, j);
     PP_TRACE(P, tb0 + 7, pp_now());

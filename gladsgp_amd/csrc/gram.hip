@@ -13,9 +13,14 @@
 // vector and beta in registers, and walks its units in order, reloading them only when the
 // (problem, row tile) changes.
 //
+// The weighted distance is taken on design vectors pre-scaled by sqrt(beta) (the row vector in
+// registers and the staged d-tile, once per problem / segment): sum_k (a'_k - b'_k)^2 with
+// a' = sqrt(beta) a costs 2 d ops per element instead of 3 d (beta >= 0, the ARD precisions);
+// the rounding of the scaled values adds at most ~2 eps s to an element (|x| <= 1, beta <= 5),
+// inside the 8 eps s Gram tolerance.
 // Roofline: 8 B written per output element + 8 d B read per row/column vector (amortised),
-// and per element ~45 fp64 VALU ops (3 d for the weighted distance, 18 for exp_neg, the
-// store address).  At n = 4096 (lower triangle, 133k column units of 64 elements) the stores
+// and per element ~37 fp64 VALU ops (2 d for the distance, 19 for exp_neg, the store
+// address).  At n = 4096 (lower triangle, 133k column units of 64 elements) the stores
 // alone take 12.3 us (5.5 TB/s) and the arithmetic alone 17 us in tools/dbg/gram_micro.hip:
 // the kernel is bound by the fp64 VALU pipe, not by HBM (profiles/r02/gram_micro.txt).
 #include "gpfit_common.h"
@@ -67,8 +72,9 @@ __global__ __launch_bounds__(256) void ardse_kernel(
   int u = (int)(total * gw / nw);
   const int u1 = (int)(total * (gw + 1) / nw);
   int cur_b = -1, cur_ti = -1;
-  double xa[D], sb = 0.0, db = 0.0;
-  const double* bb = beta;
+  double xa[D], sq[D], sb = 0.0, db = 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) sq[k] = 0.0;
   while (u < u1) {
     // one segment: units u .. u + len - 1 share the problem b and the tile (ti, tj)
     const int b = u / g.units;
@@ -77,29 +83,42 @@ __global__ __launch_bounds__(256) void ardse_kernel(
     const int len = min(kTile - c0, u1 - u);
     int ti, tj;
     tile_of(g, t, ti, tj);
-    if (b != cur_b || ti != cur_ti) {                    // this lane's row vector, beta, s, delta
-      bb = beta + (long long)b * ldbeta;
+    // every load of the segment is issued before any of them is used: the row vector (on a
+    // row-tile change), the d-tile's column vectors, and beta / s / delta (on a problem change)
+    const int j0 = tj * kTile;
+    const int jc = j0 + lane;
+    const bool cok = lane >= c0 && lane < c0 + len && jc < nb;
+    const double* src = XB + (long long)(cok ? jc : 0) * ldxb;
+    double xb_raw[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xb_raw[k] = (cok && k < d) ? src[k] : 0.0;
+    const bool new_b = b != cur_b, new_row = new_b || ti != cur_ti;
+    if (new_row) {
       const int ic = min(ti * kTile + lane, na - 1);
 #pragma unroll
       for (int k = 0; k < D; ++k) xa[k] = k < d ? XA[(long long)ic * ldxa + k] : 0.0;
+    }
+    if (new_b) {
+      // sqrt(beta) of problem b: lane k takes beta_k's root (one root per lane, in parallel),
+      // then each is broadcast to the wave through SGPRs
+      const double bl = lane < d ? beta[(long long)b * ldbeta + lane] : 0.0;
+      const double rl = __builtin_sqrt(bl);               // NaN for a negative beta
+#pragma unroll
+      for (int k = 0; k < D; ++k) sq[k] = readlane_f64(rl, k);
       sb = s[b];
       db = delta ? delta[b] : 0.0;
+    }
+    if (new_row) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) xa[k] *= sq[k];
       cur_b = b;
       cur_ti = ti;
     }
-    double bet[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) bet[k] = k < d ? bb[k] : 0.0;
-    // the d-tile: lane l stages column tj*64 + l's design vector, read back as broadcasts
-    const int j0 = tj * kTile;
+    // the d-tile: lane l stages column tj*64 + l's scaled design vector, read back as
+    // broadcasts
     __builtin_amdgcn_wave_barrier();
-    {
-      const int j = j0 + lane;
-      const bool ok = lane >= c0 && lane < c0 + len && j < nb;
-      const double* src = XB + (long long)(ok ? j : 0) * ldxb;
 #pragma unroll
-      for (int k = 0; k < D; ++k) xs[lane * D + k] = (ok && k < d) ? src[k] : 0.0;
-    }
+    for (int k = 0; k < D; ++k) xs[lane * D + k] = xb_raw[k] * sq[k];
     __builtin_amdgcn_wave_barrier();
     const int i = ti * kTile + lane;
     const int cend = min(c0 + len, cols_out - j0);      // columns this segment stores
@@ -115,7 +134,7 @@ __global__ __launch_bounds__(256) void ardse_kernel(
 #pragma unroll
         for (int k = 0; k < D; ++k) {
           const double dt = xa[k] - xb[k];
-          acc = fma(bet[k] * dt, dt, acc);
+          acc = fma(dt, dt, acc);
         }
         o[(long long)(j0 + c) * ldo] = sb * exp_neg(acc);
       }
@@ -128,7 +147,7 @@ __global__ __launch_bounds__(256) void ardse_kernel(
 #pragma unroll
         for (int k = 0; k < D; ++k) {
           const double dt = xa[k] - xb[k];
-          acc = fma(bet[k] * dt, dt, acc);
+          acc = fma(dt, dt, acc);
         }
         double v = fma(sb, exp_neg(acc), (i == j) ? db : 0.0);
         v = (row_ok && j < nb) ? v : 0.0;

@@ -38,7 +38,8 @@ constexpr int kDefaultChunkSingle = 16384;            // ... and for one GP
 //   Kt[k * mc + c] = s * exp(-sum beta (X[k] - Xs[c])^2)
 // (zero for k >= n or c >= mv).  Each thread owns one test point c (registers) and walks 32
 // k-pairs whose design rows are broadcast from LDS; a wave stores 512 contiguous bytes per
-// row k.
+// row k.  Both design vectors are pre-scaled by sqrt(beta) (beta >= 0): 2 d ops per element
+// for the distance instead of 3 d (see gram.hip for the rounding bound).
 template <int D>
 __global__ __launch_bounds__(256) void cross_kp_kernel(
     const double* __restrict__ X, int n, int ldx, const double* __restrict__ Xs, int mv,
@@ -50,14 +51,16 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
   __shared__ double xk[64][D];
   __shared__ double bs[D];
   const double* bb = beta + (long long)b * ldbeta;
-  if (threadIdx.x < D) bs[threadIdx.x] = (threadIdx.x < d) ? bb[threadIdx.x] : 0.0;
+  if (threadIdx.x < D) bs[threadIdx.x] = (threadIdx.x < d) ? __builtin_sqrt(bb[threadIdx.x]) : 0.0;
+  __syncthreads();
   for (int t = threadIdx.x; t < 64 * D; t += 256) {
     const int kk = t / D, dd = t % D, k = 2 * kp0 + kk;
-    xk[kk][dd] = (k < n && dd < d) ? X[(long long)k * ldx + dd] : 0.0;
+    xk[kk][dd] = (k < n && dd < d) ? X[(long long)k * ldx + dd] * bs[dd] : 0.0;
   }
   double xc[D];
 #pragma unroll
-  for (int dd = 0; dd < D; ++dd) xc[dd] = (c < mv && dd < d) ? Xs[(long long)c * ldxs + dd] : 0.0;
+  for (int dd = 0; dd < D; ++dd)
+    xc[dd] = (c < mv && dd < d) ? Xs[(long long)c * ldxs + dd] * bs[dd] : 0.0;
   __syncthreads();
   if (c >= mc) return;
   const double sb = s[b];
@@ -70,8 +73,8 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
 #pragma unroll
     for (int dd = 0; dd < D; ++dd) {
       const double t0 = xk[2 * kk][dd] - xc[dd], t1 = xk[2 * kk + 1][dd] - xc[dd];
-      e0 = fma(bs[dd] * t0, t0, e0);
-      e1 = fma(bs[dd] * t1, t1, e1);
+      e0 = fma(t0, t0, e0);
+      e1 = fma(t1, t1, e1);
     }
     // exp unconditionally, then select: padding rows / columns have finite (zeroed) inputs,
     // and a conditional exp costs an exec-mask branch around each call

@@ -17,6 +17,8 @@
  *    every other entry point allocate nothing;
  *  - matrices are column-major with a leading dimension (LAPACK layout), element (i,j) at
  *    A[i + j*ld]; design matrices X (n x d) are row-major with row stride ldx >= d;
+ *  - beta holds ARD precisions, beta >= 0 (the kernels take sqrt(beta); a negative entry
+ *    yields NaN, which the factorisation reports through info);
  *  - `batch` independent problems share X / Xs; per-problem operands advance by the given
  *    stride (matrices), by ldbeta (beta rows), by 1 (s, delta, s_pred, info, logdet) and by
  *    ldw / ldo (w_hat, mean, var columns);

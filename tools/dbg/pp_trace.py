@@ -54,7 +54,7 @@ us = lambda x: (x - t0) / 100.0   # noqa: E731  (100 MHz -> us)
 work = [k for k in range(nt) if tasks[k][0] != "C" and tk[k, 1] > 0]
 print(f"n={n} N={N} tasks={nt}  chain end {us(cs[N-1, 4]):.1f} us; last task end "
       f"{us(tk[work, 3].max()):.1f} us")
-ph = ["waitDP", "syrk+fill", "factor", "storeD", "waitSP", "ldP", "gemm+st", "->next"]
+ph = ["waitDP", "fill", "factor", "stD+pub", "waitSP+ldP", "gemm", "st+syrk", "->next"]
 acc = np.zeros(8)
 for j in range(N - 1):
     d = [(cs[j, q + 1] - cs[j, q]) / 100 for q in range(7)] + [(cs[j + 1, 0] - cs[j, 7]) / 100]
