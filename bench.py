@@ -396,7 +396,7 @@ def main():
     tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic, traffic_src = None, None
     chunk = args.m_chunk or 16384   # the library's default test-point chunk for one GP
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         tf = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         tj = json.load(open(tf)) if os.path.exists(tf) else {}
         if tj and n == 4096 and chunk == tj.get("m_chunk") and ml == tj.get("m", 100000):
@@ -549,6 +549,13 @@ def main_c4(args):
     K = args.steps
     value = P * m * K / elapsed
     tr_flops = float(bl) * m * K * (n * n + 4 * n)
+    traffic, traffic_src = None, None
+    tf = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_c4.json")
+    if os.path.exists(tf) and ctx.world == 1 and args.m_chunk in (0, 4096):
+        tj = json.load(open(tf))
+        if tj.get("n") == n and tj.get("batch") == P and tj.get("m") == m:
+            traffic = tj["kernels"]["trmm_pair_kernel"]["bytes_per_launch"]
+            traffic_src = "profiles/r03/pmc_traffic_c4.json (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
     tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12 if tr_ms > 0 else 0.0
     line = {
         "metric": "GP posterior predictions/sec fp64, multivariate emulator (C4: 32 PC GPs, "
@@ -565,8 +572,9 @@ def main_c4(args):
         "roofline": {"kernel": "trmm_pair_kernel (rank 0's PCs)", "bound": "mfma",
                      "achieved": round(tr_tfs, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
-                     "traffic": None, "launches": tr_cnt,
-                     "avg_launch_ms": round(tr_ms / max(tr_cnt, 1), 4)},
+                     "traffic": traffic, "traffic_source": traffic_src, "launches": tr_cnt,
+                     "avg_launch_ms": round(tr_ms / max(tr_cnt, 1), 4),
+                     "flop_per_launch": tr_flops / max(tr_cnt, 1)},
         "roofline_aux": {"potrf_inv_ms_per_step": round(p_ms / K, 4)},
         "cpu_baseline": None,
     }

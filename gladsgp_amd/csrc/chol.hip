@@ -395,7 +395,10 @@ GP_DEV void st16(lds_double* Cb, const f64x4& a, double sg) {
 // A's lower triangle holds Lt[r][c] p_c and W = Lt^-1:  L = A D^-1/2 (columns), L^-1 = D^-1/2 W
 // (rows).  Per step the dependent chain is readlane -> rcp + 2 Newton -> select -> MFMA; the
 // register-resident form with one readlane pair per row and step (and the SGPR traffic that
-// came with it) measured 8.5k cycles per leaf (tools/dbg/leaf_micro.hip).
+// came with it) measured 8.5k cycles per leaf (tools/dbg/leaf_micro.hip).  Splitting the W
+// row operations onto a second wave (multipliers handed over through LDS, a step counter)
+// measured slower inside the chain: 14.6 vs 12.4 us per 64 x 64 factor
+// (profiles/r03/pp_trace_pp4_pairs_splitleaf.txt).
 GP_DEV void leaf16(lds_double* T, lds_double* U, int o, lds_double* piv) {
   const int lane = threadIdx.x & 63;
   const int r0 = lane >> 4, c = lane & 15;
@@ -919,6 +922,16 @@ __global__ void trtri_info_kernel(int* __restrict__ info, int batch) {
 // ------------------------------------------------------------------------------------------
 constexpr int kPPMaxN = 240;          // schedule_kernel: one thread per key (4N+63 <= 1024)
 constexpr int kTChain = 0, kTL = 1, kTDP = 2, kTSP = 3, kTX = 4;
+// (LT(i,j) + LT(i+1,j) pairs sharing L_jk were tried: keyed at the second row's
+// anti-diagonal they delayed the row tiles SP(j) waits on, chain waits 7.7 vs 1.9 us per step,
+// profiles/r03/pp_trace_pp4_pairs_splitleaf.txt; removed)
+// XT tasks of the last kPPXTailRows rows stay single: they run after the chain's end (the
+// launch's tail), where a pair's doubled K loop is latency, not throughput (tail 330 vs 200 us,
+// profiles/r03/pp_trace_pp5.txt).  Splitting the tail rows' long XT sums in two (the first half
+// dequeued as soon as its inputs were) cut the tail to 194 us but slowed the chain's late phase
+// more (n = 4096 2.07 vs 1.84 ms, profiles/r03/ab_libs_pp7.log): removed.
+constexpr int kPPXTailRows = 8;
+constexpr int kTX2 = 6;     // XT pair: X_ic and X_i,c+1 (one opA stream, two opB streams)
 constexpr long long kPollBudget = 1ll << 22;   // default s_sleep polls before a wait gives up
 // gp_set_poll_budget (test / diagnostics hook): polls per wait for later launches; < 0 starts
 // every problem aborted (the deterministic abort path of the tests)
@@ -1168,13 +1181,15 @@ GP_DEV bool pp_test1(const int* f) {
   return ok != 0;
 }
 
-// One K step of a worker task: opA tile (NAT), opB tile (NAT or TRN), the two producer flags.
+// One K step of a worker task: opA tile (NAT), opB tile (NAT or TRN), the producer flags, and
+// for the paired XT2 task a third tile: its second B (X_k,c+1, TRN; absent at the first term,
+// X_c,c+1 = 0).
 struct PPTerm {
-  const double *a, *b;
-  const int *fa, *fb;
-  int lda_, ldb_, av, bv;   // av: valid rows of opA's tile; bv: valid rows of opB's (NAT)
+  const double *a, *b, *c;
+  const int *fa, *fb, *fc;
+  int lda_, ldb_, ldc_, av, bv, cv;   // av / cv: valid rows of the NAT tiles; bv: of opB (NAT)
   bool btrn;
-  bool ca, cb;              // operand tile rewritten in place during the launch: sc1 load
+  bool ca, cb, cc;          // operand tile rewritten in place during the launch: sc1 load
 };
 
 struct PPTask {
@@ -1191,7 +1206,12 @@ GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
   PPTerm u;
   u.lda_ = P.lda;
   u.ldb_ = P.lda;
+  u.ldc_ = P.lda;
   u.btrn = false;
+  u.c = nullptr;
+  u.fc = nullptr;
+  u.cv = NB;
+  u.cc = true;
   // L tiles (r, k) with r - k <= 1 pass through P partial sums in place (DP / SP tasks on any
   // XCD) before the chain writes L: read them with sc1 so no XCD's L2 serves a stale line.  Every
   // other operand tile is written once, by the XCD that alone read its old contents, and is
@@ -1213,12 +1233,19 @@ GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
     u.fb = (k == T.j) ? F + k * N + k : F + N * N + k * N + T.j;
     u.bv = NB;                               // X is zero-padded to npad: always in bounds
     u.btrn = true;
+    if (T.kind == kTX2 && k > T.j) {         // + L_ik X_k,c+1 (X_c+1,c+1 = D_c+1)
+      const int c1 = T.j + 1;
+      u.c = Xb + k * NB + (long long)c1 * NB * P.ldx;
+      u.ldc_ = P.ldx;
+      u.fc = (k == c1) ? F + k * N + k : F + N * N + k * N + c1;
+      u.cc = !P.plain;
+    }
   }
   return u;
 }
 
-// Lane-parallel readiness scan: the number of consecutive terms t0, t0+1, ... whose two input
-// flags are set (wave 0, one term per lane), at least 1 unless the problem aborted (-1).
+// Lane-parallel readiness scan: the number of consecutive terms t0, t0+1, ... whose input
+// flags are all set (wave 0, one term per lane), at least 1 unless the problem aborted (-1).
 GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -1229,7 +1256,7 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
       bool rdy = true;
       if (t < T.nterms) {
         const PPTerm u = pp_term(P, T, t);
-        rdy = pp_ldflag(u.fa) != 0 && pp_ldflag(u.fb) != 0;
+        rdy = pp_ldflag(u.fa) != 0 && pp_ldflag(u.fb) != 0 && (!u.fc || pp_ldflag(u.fc) != 0);
       }
       const unsigned long long m = __ballot(rdy);
       const int lead = (~m == 0ull) ? 64 : __builtin_ctzll(~m);
@@ -1248,48 +1275,59 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
   return r;
 }
 
-GP_DEV void pp_load_term(const PPTerm& u, OpTile& ta, OpTile& tb) {
+GP_DEV void pp_load_term(const PPTerm& u, OpTile& ta, OpTile& tb, OpTile& tc) {
   pp_load(ta, u.a, u.lda_, u.av, NB, u.ca);
   if (u.b != u.a) pp_load(tb, u.b, u.ldb_, u.bv, NB, u.cb);
+  if (u.c) pp_load(tc, u.c, u.ldc_, u.cv, NB, u.cc);
 }
 
 // Worker: accumulate the task's K steps in registers (software-pipelined: the next step's
 // operands are loaded while the current step's MFMAs run, whenever its flags are known set).
-GP_DEV bool pp_accumulate(const PPArgs& P, const PPTask& T, f64x4 (&acc)[2][2], int* abort) {
+// The paired XT2 accumulates its second output in acc2 from the third tile (staged in g_keep,
+// which only the chain uses otherwise): acc2 += L_ik X_k,c+1, sharing opA: three tile loads
+// per two tile-terms instead of four.
+GP_DEV bool pp_accumulate(const PPArgs& P, const PPTask& T, f64x4 (&acc)[2][2],
+                          f64x4 (&acc2)[2][2], int* abort) {
   Smem& sm = g_sm;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = zero4();
+    for (int nj = 0; nj < 2; ++nj) {
+      acc[mi][nj] = zero4();
+      acc2[mi][nj] = zero4();
+    }
   if (T.nterms == 0) return true;
-  OpTile ta, tb;
+  OpTile ta, tb, tc;
   int avail = pp_ready(P, T, 0, abort);      // terms [0, avail) are ready
   if (avail < 0) return false;
   PPTerm u = pp_term(P, T, 0);
-  pp_load_term(u, ta, tb);
+  pp_load_term(u, ta, tb, tc);
   for (int t = 0; t < T.nterms; ++t) {
     const bool same = u.b == u.a;
     const bool trn = u.btrn;
-    __syncthreads();                                   // the previous MFMAs have read As / Bs
+    const bool third = u.c != nullptr;
+    __syncthreads();                                   // the previous MFMAs have read the tiles
     store_op<false>(sm.As, ta);
     if (!same) {
       if (trn) store_op<true>(sm.Bs, tb);
       else store_op<false>(sm.Bs, tb);
     }
+    if (third) store_op<true>(g_keep, tc);
     __syncthreads();
     const bool more = t + 1 < T.nterms;
     const bool pre = more && t + 1 < avail;
     if (pre) {
       u = pp_term(P, T, t + 1);
-      pp_load_term(u, ta, tb);
+      pp_load_term(u, ta, tb, tc);
     }
     mma64_add(sm.As, same ? sm.As : sm.Bs, acc);
+    if (third) mma64_add(sm.As, g_keep, acc2);
     if (more && !pre) {
       const int r = pp_ready(P, T, t + 1, abort);
       if (r < 0) return false;
       avail = t + 1 + r;
       u = pp_term(P, T, t + 1);
-      pp_load_term(u, ta, tb);
+      pp_load_term(u, ta, tb, tc);
     }
   }
   return true;
@@ -1335,7 +1373,8 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   int* abort = F + 2 * N * N + 2 * N;
   if (pp_ldflag(abort)) return;
   double* Ab = P.A + T.b * P.sA;
-  f64x4 acc[2][2];
+  double* Xb = P.X + T.b * P.sX;
+  f64x4 acc[2][2], acc2[2][2];
   PP_MARK(P, 20 + T.kind, T.i * 1000 + T.j);
   PP_STALL_RESET();
   const long long tr = (long long)T.idx * 6;   // trace slots of this task (trace build)
@@ -1344,13 +1383,15 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   PP_TRACE(P, tr + 4, T.kind | (T.b << 4));
   PP_TRACE(P, tr + 5, T.i | (T.j << 16));
   auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
+  auto xtile = [&](int r, int c) { return Xb + r * NB + (long long)c * NB * P.ldx; };
   auto rv = [&](int r) { return min(NB, P.n - r * NB); };
+  const bool xt = T.kind == kTX || T.kind == kTX2;
   // the task's own A tile (DP / SP: the chain's partial-sum tile; LT: A_ij), in flight from
   // here until the epilogue
   const int ar = T.kind == kTDP ? T.j : (T.kind == kTSP ? T.j + 1 : T.i);
   OpTile ta;
-  if (T.kind != kTX) pp_load(ta, atile(ar, T.j), P.lda, rv(ar), T.kind == kTL ? NB : rv(T.j));
-  if (!pp_accumulate(P, T, acc, abort)) return;
+  if (!xt) pp_load(ta, atile(ar, T.j), P.lda, rv(ar), T.kind == kTL ? NB : rv(T.j));
+  if (!pp_accumulate(P, T, acc, acc2, abort)) return;
   PP_MARK(P, 30 + T.kind, T.i * 1000 + T.j);
   PP_TRACE(P, tr + 2, pp_now());
   // slot 0: workgroup | ticks polled before the K loop finished << 8
@@ -1385,7 +1426,7 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
     PP_TRACE(P, tr + 3, pp_now());
     return;
   }
-  // XT: X_ic = -D_i S, S = acc
+  // XT: X_ic = -D_i S, S = acc (XT2: X_i,c+1 = -D_i S2, S2 = acc2), through g_keep
   __syncthreads();
   acc_to_lds_rm(sm.Bs, acc);                            // Bs[p][cc] = S[p][cc]
   if (!pp_wait1(F + T.i * N + T.i, abort, P.budget)) return;
@@ -1398,11 +1439,24 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
   __syncthreads();
   mma64(sm.As, sm.Bs, acc);
   __syncthreads();
-  acc_to_lds(sm.As, acc);
+  acc_to_lds(g_keep, acc);
   __syncthreads();
-  double* Xb = P.X + T.b * P.sX;
-  pp_store_cm(Xb + T.i * NB + (long long)T.j * NB * P.ldx, P.ldx, sm.As, NB, NB, true);
-  pp_publish(F + N * N + T.i * N + T.j);
+  pp_store_cm(xtile(T.i, T.j), P.ldx, g_keep, NB, NB, true);
+  if (T.kind == kTX2) {
+    acc_to_lds_rm(sm.Bs, acc2);                         // (the barrier above: Bs read)
+    __syncthreads();                                    // ... and every wave's g_keep reads
+    mma64(sm.As, sm.Bs, acc2);
+    __syncthreads();
+    acc_to_lds(g_keep, acc2);
+    __syncthreads();
+    pp_store_cm(xtile(T.i, T.j + 1), P.ldx, g_keep, NB, NB, true);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pp_stflag(F + N * N + T.i * N + T.j, 1);
+    if (T.kind == kTX2) pp_stflag(F + N * N + T.i * N + T.j + 1, 1);
+  }
   PP_MARK(P, 41, T.i * 1000 + T.j);
   PP_TRACE(P, tr + 3, pp_now());
 }
@@ -1592,7 +1646,9 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
 // W = 4: n = 4096 1.855-1.857 ms median vs 1.880-1.890 at W = 6 and 1.896-1.909 at 8, batch 32
 // unchanged (profiles/r02/ab_pp_lead_xd.log, XT delay 6 / 8 / 11 equal within noise).
 constexpr int kPPLead = 4;
-constexpr int kPPLeadBlocked = 4 * kPPLead + 2;   // per-problem bound on blocked early tasks
+// per-problem bound on early tasks blocked on tasks not yet dequeued: W DP, W SP and 2W band
+// LT in the 4W positions ahead, + 2 positions for the LT pairs keyed at their second row
+constexpr int kPPLeadBlocked = 4 * kPPLead + 6;
 constexpr int kPPBand = 3;
 constexpr int kPPXDelay = 8;   // XT tasks: 8 chain steps after the late LT tasks of their row
 
@@ -1603,24 +1659,32 @@ constexpr int kPPXDelay = 8;   // XT tasks: 8 chain steps after the late LT task
 // section comment).  Shared by the schedule kernel (count + emit) and the host's task count.
 template <typename F>
 GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, int xd, F&& f) {
+  // late tasks of this position first (K = t - 4W): a late task can be an input of an early
+  // task of the same position, never the other way round
+  const int K = t - 4 * lead;
+  if (K >= 0) {
+    const int KX = K - 4 * xd;
+    if (inv && KX >= 0 && KX % 4 == 2 && (KX - 2) / 4 >= 1 && (KX - 2) / 4 <= N - 1) {
+      const int i = (KX - 2) / 4;
+      if (i + kPPXTailRows < N) {                              // pairs (c, c+1), longest first
+        for (int c = 0; c + 1 < i; c += 2) f(kTX2, i, c);
+        if (i & 1) f(kTX, i, i - 1);
+      } else {                                                 // the last rows: singles
+        for (int c = 0; c < i; ++c) f(kTX, i, c);
+      }
+    }
+    if (K % 2 == 0) {                                          // late LT
+      const int s = K / 2;
+      const int jmin = s - (N - 1) > 0 ? s - (N - 1) : 0;
+      for (int j = (s - kPPBand - 1) / 2; j >= jmin && s >= kPPBand + 1; --j) f(kTL, s - j, j);
+    }
+  }
   if (t % 4 == 2 && (t + 2) / 4 >= 2 && (t + 2) / 4 <= N - 1) f(kTDP, 0, (t + 2) / 4);
   if (t % 4 == 1 && (t - 1) / 4 >= 1 && (t - 1) / 4 <= N - 2) f(kTSP, (t - 1) / 4 + 1, (t - 1) / 4);
   if (t % 2 == 0 && t >= 4) {                                  // band LT on anti-diagonal s
     const int s = t / 2;
     const int jmin = (s - kPPBand + 1) / 2 > s - (N - 1) ? (s - kPPBand + 1) / 2 : s - (N - 1);
     for (int j = (s - 2) / 2; j >= jmin && j >= 0; --j) f(kTL, s - j, j);
-  }
-  const int K = t - 4 * lead;
-  if (K < 0) return;
-  const int KX = K - 4 * xd;
-  if (inv && KX >= 0 && KX % 4 == 2 && (KX - 2) / 4 >= 1 && (KX - 2) / 4 <= N - 1) {
-    const int i = (KX - 2) / 4;
-    for (int c = 0; c < i; ++c) f(kTX, i, c);                  // longest (most K steps) first
-  }
-  if (K % 2 == 0) {                                            // late LT singles
-    const int s = K / 2;
-    const int jmin = s - (N - 1) > 0 ? s - (N - 1) : 0;
-    for (int j = (s - kPPBand - 1) / 2; j >= jmin && s >= kPPBand + 1; --j) f(kTL, s - j, j);
   }
 }
 
@@ -1780,7 +1844,7 @@ static PPScratch pp_scratch(int n, int batch, bool inv) {
   PPScratch s;
   const int N = gp_ceil_div(n, NB);
   s.ntasks = pp_task_count(N, inv) * batch;
-  s.fstride = ((2 * N * N + 2 * N + 1 + 31) / 32) * 32;
+  s.fstride = ((2 * N * N + 2 * N + 1 + 31) / 32) * 32;   // FL, FX, DPF, SPF, abort
   s.task_bytes = ((size_t)s.ntasks * sizeof(int2) + 255) / 256 * 256;
   s.flag_bytes = ((256 + (size_t)batch * s.fstride * sizeof(int)) + 255) / 256 * 256;
   return s;

@@ -45,7 +45,7 @@ t = trace.cpu().numpy()
 tk = t[: nt * SL].reshape(nt, SL).astype(np.float64)
 kinds_raw = t[: nt * SL].reshape(nt, SL)[:, 4] & 15
 ij = t[: nt * SL].reshape(nt, SL)[:, 5]
-KN = {1: "L", 2: "DP", 3: "SP", 4: "X"}
+KN = {1: "L", 2: "DP", 3: "SP", 4: "X", 6: "X2"}
 tasks = [("C", 0, 0) if kinds_raw[k] == 0 else (KN[int(kinds_raw[k])], int(ij[k] & 0xffff),
                                                 int(ij[k] >> 16)) for k in range(nt)]
 cs = t[nt * SL:].reshape(N, 8).astype(np.float64)
@@ -69,7 +69,9 @@ for k in work:
     dur.setdefault(kd, []).append((tk[k, 2] - tk[k, 1]) / 100)
     ep.setdefault(kd, []).append((tk[k, 3] - tk[k, 2]) / 100)
     stall.setdefault(kd, []).append((int(t[k * SL]) >> 8) / 100)
-    terms.setdefault(kd, []).append(j if kd in ("L", "SP") else j - 1 if kd == "DP" else i - j)
+    terms.setdefault(kd, []).append(      # 64^3 tile-terms (a pair does two per K step)
+        j if kd in ("L", "SP") else j - 1 if kd == "DP" else 2 * (i - j) - 1 if kd == "X2"
+        else i - j)
 for kd, v in dur.items():
     nterm = np.sum(terms[kd])
     print(f"{kd}: {len(v)} tasks, accumulate mean {np.mean(v):.1f} us max {np.max(v):.1f}, "
@@ -91,7 +93,7 @@ for k in work:
     end = us(tk[k, 3])
     if kd == "L":
         rowsL[i] = max(rowsL.get(i, 0), end)
-    if kd == "X":
+    if kd in ("X", "X2"):
         rowsX[i] = max(rowsX.get(i, 0), end)
 print("row: L done / X done (us)")
 for r in range(0, N, 4):

@@ -1,17 +1,19 @@
 #!/bin/bash
 # HBM traffic per kernel from PMC counters (separate passes: FETCH_SIZE, WRITE_SIZE).
+#   tools/pmc_traffic.sh [c3|c4]   -> gpurun_out/pmc_traffic.json | pmc_traffic_c4.json
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
+WL=${1:-c3}
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c -d $R/gpurun_out/pmc_$c -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/pmc_$c.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --pmc $c -d $R/gpurun_out/pmc_${WL}_$c -o run --output-format csv -- python3 $R/bench.py --workload $WL --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/pmc_${WL}_$c.log 2>&1 || exit 1
 done
-python3 - "$R" <<'PY'
+python3 - "$R" "$WL" <<'PY'
 import csv, glob, json, sys, collections
-R = sys.argv[1]
+R, WL = sys.argv[1], sys.argv[2]
 means = collections.defaultdict(dict)
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    f = glob.glob(f"{R}/gpurun_out/pmc_{c}/**/*counter_collection.csv", recursive=True)
+    f = glob.glob(f"{R}/gpurun_out/pmc_{WL}_{c}/**/*counter_collection.csv", recursive=True)
     if not f:
         print("no counter csv for", c, glob.glob(f"{R}/gpurun_out/pmc_{c}/**/*", recursive=True)); continue
     rows = list(csv.DictReader(open(f[0])))
@@ -25,23 +27,27 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
 # (gfx950 reports half the bytes of 16-B/lane streams, MI355X_MICROARCH.md HBM section) + WRITE
 t = means.get("trmm_pair_kernel", {})
 if t:
-    n, m, chunk = 4096, 100000, 16384
-    L = 8.0 * 4096 * 4097 / 2 + 0.0      # L^-1 lower triangle
-    kt = 8.0 * 4096 * m / 7              # mean Kt chunk per launch (7 launches per 100k)
+    if WL == "c3":
+        n, m, chunk, batch, launches = 4096, 100000, 16384, 1, 7
+    else:                                # C4: 32 GPs, n = 1024, 4096-point chunks
+        n, m, chunk, batch, launches = 1024, 100000, 4096, 32, 25
+    L = 8.0 * n * (n + 1) / 2 * batch    # L^-1 lower triangles
+    kt = 8.0 * n * m / launches * batch  # mean Kt chunk per launch
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of "
                      "`bench.py --steps 2 --warmup 1 --no-cpu`, MI355X (tools/pmc_traffic.sh)",
            "correction": "FETCH_SIZE x2 (gfx950 tallies 16-B/lane streams at half their bytes); "
                          "WRITE_SIZE as reported",
-           "m_chunk": chunk, "m": m,
+           "workload": WL, "m_chunk": chunk, "m": m, "n": n, "batch": batch,
            "kernels": {"trmm_pair_kernel": {
                "fetch_kb_raw": t.get("FETCH_SIZE"), "write_kb": t.get("WRITE_SIZE"),
                "bytes_per_launch": 1024.0 * (2 * t.get("FETCH_SIZE", 0) + t.get("WRITE_SIZE", 0)),
                "algorithmic_bytes_per_launch": L + kt,
-               "note": "per-dispatch mean over the 7 launches of a step; algorithmic = L^-1 lower "
-                       "triangle + the launch's mean Kt chunk"}}}
+               "note": f"per-dispatch mean over the {launches} launches of a step; algorithmic = "
+                       "L^-1 lower triangle(s) + the launch's mean Kt chunk"}}}
     for k, v in means.items():
         if k != "trmm_pair_kernel":
             out["kernels"][k] = {"fetch_kb_raw": v.get("FETCH_SIZE"), "write_kb": v.get("WRITE_SIZE")}
-    json.dump(out, open(f"{R}/gpurun_out/pmc_traffic.json", "w"), indent=1)
+    name = "pmc_traffic.json" if WL == "c3" else f"pmc_traffic_{WL}.json"
+    json.dump(out, open(f"{R}/gpurun_out/{name}", "w"), indent=1)
     print("trmm_pair_kernel bytes/launch", out["kernels"]["trmm_pair_kernel"]["bytes_per_launch"])
 PY
