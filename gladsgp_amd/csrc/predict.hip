@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
   }
 }
 
-// One 128x128 tile of V = Linv * Kt per block, 4 waves in 2x2 (64x64 each = 4x4 MFMA tiles).
+// One 128x128 tile of V = Linv * Kt per block, 4 waves in 2 wave rows x 2 wave columns: a wave
+// owns four 16-row MFMA row tiles (dealt in a snake, trmm_rtile) x 64 columns (4x4 MFMA tiles).
 // Operands stream straight into LDS with global_load_lds (16 B per lane), double-buffered:
 //   A step (16 k x 128 rows of L^-1): 16 rows of 1 KB, row pitch 1152 B (lanes 0-15 / 16-31
 //     of a fragment read land 32 banks apart: conflict-free)
@@ -103,27 +104,33 @@ GP_DEV void glds16(const double* g, double* l) {
                                    (void __attribute__((address_space(3)))*)l, 16, 0, 0);
 }
 
-// One staged K step (16 k) of a wave's 64x64 sub-tile.  TAIL: the step lies in the tile's
-// diagonal block of L^-1, where the wave's 16-row MFMA tile mi only meets nonzero L^-1 entries
-// when mi >= lo (lo = the step's offset into the wave's own 64-row diagonal, in 16-k steps).
-// The skipped products are exact zeros (L^-1 is zero above the diagonal), so the sums are
-// unchanged and the SIMD goes to the co-resident block's waves instead.
+// The 16-row MFMA tiles of a 128-row tile are dealt to the two wave rows in a snake,
+// wave row wr owning tiles {wr, 3-wr, 4+wr, 7-wr}: inside the diagonal block, where tile r only
+// meets nonzero L^-1 in the steps t <= r, both wave rows then run 18 of the block's 32
+// tile-steps, instead of 10 and 26 with contiguous halves -- a step's barrier waits for the
+// busier row, so the diagonal block took 6.5 steps' time for 4.5 steps of work.
+GP_DEV constexpr int trmm_rtile(int mi, int wr) { return 2 * mi + ((mi & 1) ? 1 - wr : wr); }
+
+// One staged K step (16 k) of a wave's four 16 x 64 MFMA row tiles.  TAIL: the step is step t
+// of the tile's diagonal block of L^-1, where row tile r only meets nonzero L^-1 entries when
+// r >= t.  The skipped products are exact zeros (L^-1 is zero above the diagonal), so the sums
+// are unchanged and the SIMD goes to the co-resident block's waves instead.
 template <bool TAIL>
 GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__ Bs,
-                       f64x4 (&acc)[4][4], int wr, int wc, int li, int lk, int lo) {
+                       f64x4 (&acc)[4][4], int wr, int wc, int li, int lk, int t) {
 #pragma unroll
   for (int k4 = 0; k4 < BK / 4; ++k4) {
     const int k = k4 * 4 + lk;
     double a[4], bb[4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
-      if (!TAIL || mi >= lo) a[mi] = As[k * APITCH + wr * 64 + mi * 16 + li];
+      if (!TAIL || trmm_rtile(mi, wr) >= t) a[mi] = As[k * APITCH + trmm_rtile(mi, wr) * 16 + li];
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj)
       bb[nj] = Bs[k * BC + wc * 64 + nj * 16 + li];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
-      if (TAIL && mi < lo) continue;
+      if (TAIL && trmm_rtile(mi, wr) < t) continue;
 #pragma unroll
       for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = mfma16x16x4(a[mi], bb[nj], acc[mi][nj]);
     }
@@ -192,20 +199,20 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
       double* cur = smem + (s & 1) * STAGE;
       if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
       else if (pass + 1 < npass) issue(Lb + Ilo * BI, 0, smem);   // next tile's first stage
-      const int lo = (s - s_diag) - 4 * wr;   // wave-uniform
-      if (lo < 4) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, lo);
+      const int t = s - s_diag;               // the wave's last row tile is 7 - wr
+      if (t <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
 
     // epilogue in stage buffer 1 (buffer 0 may hold the next tile's first stage)
     double* red = smem + STAGE;
-    const double* zb = z + (long long)b * npad + I * BI + wr * 64;
+    const double* zb = z + (long long)b * npad + I * BI;
     double zr[4][4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) zr[mi][r] = zb[mi * 16 + lk + 4 * r];
+      for (int r = 0; r < 4; ++r) zr[mi][r] = zb[trmm_rtile(mi, wr) * 16 + lk + 4 * r];
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) {
       double sm = 0.0, sv = 0.0;
