@@ -57,20 +57,32 @@ def _offsets(counts: list[int]) -> list[int]:
 
 class LinvPacker:
     """L^-1's nonzero part (column c of the column-major buffer from row c on) as one flat
-    vector: what the broadcast carries (about half the padded square)."""
+    vector: what the broadcast carries (about half the padded square), followed by one slot
+    holding the factorisation's info, so every receiver learns whether the factor it got is
+    valid from the same collective (a rank-0-only raise before the broadcast would leave the
+    other ranks waiting in it)."""
 
     def __init__(self, npad: int, device):
         tri = torch.triu_indices(npad, npad, device=device)   # (c, r), r >= c of the [c][r] view
         self.flat = tri[0] * npad + tri[1]
         self.numel = int(self.flat.numel())
 
-    def pack(self, linv_buf: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-        return torch.index_select(linv_buf.reshape(-1), 0, self.flat, out=out)
+    def buffer(self, device) -> torch.Tensor:
+        return torch.zeros(self.numel + 1, dtype=F64, device=device)
+
+    def pack(self, linv_buf: torch.Tensor, info: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        torch.index_select(linv_buf.reshape(-1), 0, self.flat, out=out[: self.numel])
+        out[self.numel:].copy_(info.reshape(1).to(F64))
+        return out
 
     def unpack(self, packed: torch.Tensor, linv_buf: torch.Tensor) -> torch.Tensor:
         """Scatter into a buffer whose upper triangle and padding are already zero."""
-        linv_buf.view(-1).index_copy_(0, self.flat, packed)
+        linv_buf.view(-1).index_copy_(0, self.flat, packed[: self.numel])
         return linv_buf
+
+    def info(self, packed: torch.Tensor) -> torch.Tensor:
+        """The sender's info (device, int32, shape (1,))."""
+        return packed[self.numel:].to(torch.int32)
 
 
 def _wire_bcast(ctx: gdist.Context, t: torch.Tensor, async_op: bool):
@@ -129,16 +141,17 @@ def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta,
         info = torch.zeros(1, dtype=torch.int32, device=dev)
         logdet = torch.zeros(1, dtype=F64, device=dev)
         packer = LinvPacker(npad, dev)
-        packed = torch.empty(packer.numel, dtype=F64, device=dev)
+        packed = packer.buffer(dev)
         if rank == 0:
             G = kernels.gram(X, beta, s, delta)
             ch = kernels.cholesky_inverse(G)
-            if check:
-                ch.check()
-            packer.pack(ch.linv_buf, packed)
+            packer.pack(ch.linv_buf, ch.info, packed)
         _wire_bcast(ctx, packed, async_op=False)
+        if check:                                  # every rank raises alike (rank 0's info)
+            kernels.check_info(packer.info(packed))
         if rank != 0:
             packer.unpack(packed, linv)
+            info.copy_(packer.info(packed))
             ch = kernels.Cholesky(n, None, linv, info, logdet)
         if hi > lo:
             kernels.predict(ch, X, Xl, beta, s, s_pred, w, m_chunk=m_chunk, workspace=workspace,
@@ -230,8 +243,9 @@ class PipelinedPredictor:
         self.info = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.logdet = torch.zeros(1, dtype=F64, device=self.dev)
         self.packer = LinvPacker(npad, self.dev)
-        self.packed = [torch.empty(self.packer.numel, dtype=F64, device=self.dev)
-                       for _ in range(2)]
+        self.packed = [self.packer.buffer(self.dev) for _ in range(2)]
+        # the first nonzero info among the GPs predicted so far (device; read by check())
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.out = torch.empty((2, max(self.ml, 1)), dtype=F64, device=self.dev)
         self.ws = kernels.Workspace()
         self.pws = kernels.Workspace()
@@ -260,7 +274,7 @@ class PipelinedPredictor:
 
     def _bcast(self, slot: int):
         if self.rank == 0:
-            self.packer.pack(self.linv[slot], self.packed[slot])
+            self.packer.pack(self.linv[slot], self.info, self.packed[slot])
         if self.world == 1:
             return None
         return _wire_bcast(self.ctx, self.packed[slot], async_op=True)
@@ -288,6 +302,8 @@ class PipelinedPredictor:
             self.pending.wait()
         if self.rank != 0 and self.world > 1:
             self.packer.unpack(self.packed[cur], self.linv[cur])
+        got = self.packer.info(self.packed[cur])
+        self.status.copy_(torch.where(self.status != 0, self.status, got))
         b, s, _, sp, w = self.gps[cur]
         ch = kernels.Cholesky(self.n, None, self.linv[cur], self.info, self.logdet)
         if self.ml:
@@ -300,8 +316,17 @@ class PipelinedPredictor:
         self.k = k + 1
         return res
 
-    def finish(self) -> None:
-        """Wait for an outstanding broadcast (after the last ``step``)."""
+    def finish(self, check: bool = True) -> None:
+        """Wait for an outstanding broadcast (after the last ``step``); with ``check``, raise
+        (on every rank alike) if any GP predicted so far had a failed factorisation: the steps
+        themselves never synchronise with the host."""
         if self.pending is not None:
             self.pending.wait()
             self.pending = None
+        if check:
+            self.check()
+
+    def check(self) -> None:
+        """Raise for the first failed factorisation among the GPs predicted so far
+        (:func:`kernels.check_info`; synchronises)."""
+        kernels.check_info(self.status)

@@ -143,13 +143,15 @@ def _points_worker(rank, world, port, results):
         npad = 8
         full = torch.tril(torch.arange(1.0, npad * npad + 1, dtype=torch.float64)
                           .reshape(npad, npad)).T.contiguous().reshape(1, npad, npad)
+        # together with rank 0's factorisation info, so every rank can raise alike
         pk = LinvPacker(npad, torch.device("cpu"))
-        packed = torch.empty(pk.numel, dtype=torch.float64)
+        packed = pk.buffer(torch.device("cpu"))
         if rank == 0:
-            pk.pack(full, packed)
+            pk.pack(full, torch.tensor([3], dtype=torch.int32), packed)
         gdist.broadcast_(ctx, packed)
         got = pk.unpack(packed, torch.zeros((1, npad, npad), dtype=torch.float64))
-        ok_l = bool(torch.equal(got, full)) and pk.numel == npad * (npad + 1) // 2
+        ok_l = (bool(torch.equal(got, full)) and pk.numel == npad * (npad + 1) // 2
+                and pk.info(packed).tolist() == [3])
         results[rank] = (ok_p, ok_l)
     finally:
         dist.destroy_process_group()

@@ -180,6 +180,26 @@ def _pipe_worker(rank, world, port, results):
             else:
                 ok_modes[key] = r is None
         out["modes"] = ok_modes
+        # a failed factorisation raises on every rank alike (rank 0's info travels with the
+        # broadcast): predict_sharded at once, PipelinedPredictor at finish()
+        dbad = torch.tensor([-2.0], dtype=torch.float64, device=dev)   # diagonal 1 - 2 < 0
+        raised = {}
+        try:
+            predict_sharded(ctx, Xd, Xsd, betas[2], sd, dbad, sd, yd, mode="broadcast",
+                            counts=split_counts(m, world, 3000.0))
+            raised["sharded"] = False
+        except ValueError:
+            raised["sharded"] = True
+        pp2 = PipelinedPredictor(ctx, Xd, Xsd, yd, counts=pp.counts)
+        pp2.start(gps[0])
+        for g in ((betas[1], sd, dbad, sd), gps[2], None):
+            pp2.step(g)
+        try:
+            pp2.finish()
+            raised["pipeline"] = False
+        except ValueError:
+            raised["pipeline"] = True
+        out["raised"] = raised
         torch.cuda.synchronize()
     except Exception:  # noqa: BLE001 - reported to the parent
         import traceback
@@ -193,7 +213,8 @@ def test_two_ranks_pipelined_and_sharded_single_gp():
     """gladsgp_amd.sharded (SURVEY §8e single-output GP) with two ranks on the one GPU:
     PipelinedPredictor (rank 0 factorises GP k+1 and broadcasts L^-1 while both ranks predict
     GP k on their blocks; consecutive GPs differ) equals a direct computation of every GP bit
-    for bit, and predict_sharded matches one rank doing all m in both factorisation modes."""
+    for bit, predict_sharded matches one rank doing all m in both factorisation modes, and a
+    non-positive-definite GP raises on both ranks (no rank left waiting in a collective)."""
     world = 2
     mgr = mp.Manager()
     results = mgr.dict()
@@ -203,6 +224,7 @@ def test_two_ranks_pipelined_and_sharded_single_gp():
         assert "error" not in res, res.get("error")
         assert res["pipe"], res
         assert all(res["modes"].values()), res["modes"]
+        assert res["raised"] == {"sharded": True, "pipeline": True}, res["raised"]
     counts = results[0]["counts"]
     assert sum(counts) == 40000 and len(counts) == 2 and 0 < counts[0] <= counts[1]
 
