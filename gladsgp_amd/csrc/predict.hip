@@ -302,7 +302,7 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
 // between the factorisation and the first TRMM (profiles/r02/step_timeline_f2d.txt).
 //   pass 1: block (rb, kt) forms row block rb's (64 rows) product with column tile kt (kZT
 //           = 128 columns; tiles on or below the diagonal only: ~1056 blocks at n = 4096),
-//           4 waves x 32 columns, 8 loads in flight per lane, into zp[kt][r];
+//           4 waves x 32 columns, all 32 loads in flight per lane, into zp[kt][r];
 //   pass 2: z[r] = sum over kt = 0 .. last tile of r's row block of zp[kt][r], in tile order.
 // Every row r < npad is written (rows >= n are 0: L^-1 is zero-padded).  zp (batch *
 // ceil(npad / kZT) * npad doubles, 1 MB per problem at n = 4096) is its own workspace region.
@@ -321,14 +321,20 @@ __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict
   const double* wb = w + (long long)b * ldw;
   const int kb = k0 + wv * kZW;
   const int ke = min(kb + kZW, min(n, rb + 64));  // L^-1 is zero right of the diagonal
+  // all of the wave's kZW column loads issued before the first FMA (one latency round instead
+  // of kZW / 8); the sums run in the same order as with 8 loads in flight, so z is unchanged
+  double lv[kZW], wk[kZW];
+#pragma unroll
+  for (int j = 0; j < kZW; ++j) {
+    const bool ok = kb + j < ke;
+    lv[j] = ok ? L[(long long)(kb + j) * ld] : 0.0;
+    wk[j] = ok ? wb[kb + j] : 0.0;
+  }
   double acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.0;
-  for (int k = kb; k < ke; k += 8) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (k + j < ke) acc[j] = fma(L[(long long)(k + j) * ld], wb[k + j], acc[j]);
-  }
+  for (int j = 0; j < kZW; ++j) acc[j & 7] = fma(lv[j], wk[j], acc[j & 7]);
   __shared__ double red[4][64];
   red[wv][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
