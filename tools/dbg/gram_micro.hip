@@ -1,6 +1,7 @@
 // Microbenchmark (debug only): what bounds the lower-triangle Gram build at n = 4096?
 // Variants over the same unit ranges as gram.hip's ardse_kernel: MODE 0 store-only (constant
-// value), 1 compute-only (exp + distance, a checksum store per wave), 2 both; lane = row,
+// value), 1 compute-only (exp + distance, a checksum store per wave), 2 both, 3 both with the
+// library's sqrt(beta)-prescaled distance (2 d ops per element instead of 3 d); lane = row,
 // 512-B column segments, 64 x 64 tiles.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -38,7 +39,10 @@ __global__ __launch_bounds__(256) void k(const double* X, int n, double* out, in
         const double* xb = xs + c * 8;
         double acc = 0.0;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) { const double dt = xa[q] - xb[q]; acc = fma(bet[q] * dt, dt, acc); }
+        for (int q = 0; q < 8; ++q) {
+          const double dt = xa[q] - xb[q];
+          acc = MODE == 3 ? fma(dt, dt, acc) : fma(bet[q] * dt, dt, acc);
+        }
         v = exp_neg(acc);
       }
       if (MODE == 1) chk += v;
@@ -60,13 +64,14 @@ int main() {
   hipMemcpy(X, hX.data(), hX.size() * 8, hipMemcpyHostToDevice);
   hipEvent_t a, b;
   hipEventCreate(&a); hipEventCreate(&b);
-  for (int mode = 0; mode < 3; ++mode)
+  for (int mode = 0; mode < 4; ++mode)
     for (int bpc : {2, 4, 7, 8}) {
       const int grid = 256 * bpc;
       auto run = [&] {
         if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(grid), dim3(256), 0, 0, X, n, G, total, 0);
         if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(grid), dim3(256), 0, 0, X, n, G, total, 0);
         if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(grid), dim3(256), 0, 0, X, n, G, total, 0);
+        if (mode == 3) hipLaunchKernelGGL(k<3>, dim3(grid), dim3(256), 0, 0, X, n, G, total, 0);
       };
       for (int r = 0; r < 3; ++r) run();
       hipEventRecord(a);
@@ -75,7 +80,8 @@ int main() {
       hipEventSynchronize(b);
       float ms; hipEventElapsedTime(&ms, a, b);
       printf("mode %d (%s) bpc %d: %.2f us/launch\n", mode,
-             mode == 0 ? "store only" : mode == 1 ? "compute only" : "both", bpc, ms * 1e3 / 20);
+             mode == 0 ? "store only" : mode == 1 ? "compute only" : mode == 2 ? "both"
+             : "both, prescaled 2d distance", bpc, ms * 1e3 / 20);
     }
   // the library kernel itself (lower triangle, as gp_fit_predict / gp_loglik build it)
   double *beta, *sv, *dv;
