@@ -184,11 +184,12 @@ class GPUSampler:
     """Component-wise Metropolis over the P PC-GPs of one emulator, all state on the device.
 
     One sweep is ~11 batched gp_loglik calls plus elementwise proposal / accept work: a few
-    hundred small launches.  With ``use_graph`` (or GPFIT_MCMC_GRAPH=1) the sweep is captured
-    once as a HIP graph (torch.cuda.CUDAGraph) over static buffers -- chain state, uniforms,
-    step sizes, counters -- and replayed.  Measured at n=512, P=8 the sweep is GPU-bound (11
-    small potrf critical paths) and graph replay was slower (6.9 vs 5.5 ms per sweep), so the
-    default is eager stream-ordered launches; both paths run the same in-place sweep.
+    hundred small launches.  By default (``use_graph`` None; GPFIT_MCMC_GRAPH=0 opts out) the
+    sweep is captured once as a HIP graph (torch.cuda.CUDAGraph) over static buffers -- chain
+    state, uniforms, step sizes, counters -- and replayed: at the timing.csv configuration
+    (n = 512, P = 8) 3.75 vs 4.04-4.26 ms per sweep eager, the fit 5.0-5.4 vs 5.7-6.3 s
+    (profiles/r03/ab_mcmc_graph.log; round 2 measured the opposite while the factorisation
+    still allocated its scratch inside every call).  Both paths run the same in-place sweep.
     """
 
     def __init__(self, X: torch.Tensor, w_hat: torch.Tensor, LamSim: torch.Tensor,
@@ -210,7 +211,7 @@ class GPUSampler:
         self.steps = {k: self._t(getattr(params, k).mcmcStepParam) for k in ModelParams.names}
         self.lp = torch.zeros(1, dtype=F64, device=self.dev)            # log posterior
         if use_graph is None:
-            use_graph = os.environ.get("GPFIT_MCMC_GRAPH", "0") == "1"
+            use_graph = os.environ.get("GPFIT_MCMC_GRAPH", "1") == "1"
         self.use_graph = use_graph and self.dev.type == "cuda"
         self.graph = None
         self.st = None

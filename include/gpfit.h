@@ -344,8 +344,9 @@ int gp_profile_read(int id, int* count, double* total_ms, double* max_ms);
  * polls a wait of the persistent factorisation makes before it gives up and reports info = -1
  * for the launches enqueued afterwards.  polls > 0 sets it, 0 restores the default (2^22, far
  * beyond any legitimate wait), < 0 makes every later factorisation start with its problems
- * given up (info = -1 deterministically: the tests of the internal-error path).  Returns the
- * previous setting. */
+ * given up (info = -1 deterministically: the tests of the internal-error path).  The value
+ * is read when a factorisation is enqueued, so a captured HIP graph keeps the one it was
+ * captured with.  Returns the previous setting. */
 long long gp_set_poll_budget(long long polls);
 
 #ifdef __cplusplus

@@ -123,15 +123,21 @@ def test_loglik_internal_error_is_nan_and_sticky(dev):
     ws.check_status()
 
 
-def test_sampler_raises_on_internal_error(dev):
+@pytest.mark.parametrize("graph", [False, True])
+def test_sampler_raises_on_internal_error(dev, graph):
+    """Eager sweeps, and a captured sweep graph (the default): kernel arguments, the preset
+    abort included, are frozen when the graph is captured, so the graph case captures after
+    gp_set_poll_budget(-1)."""
     from gladsgp_amd import _capi, kernels, mcmc
     lib = _capi.lib()
     rng = np.random.default_rng(7)
     n, P, d = 200, 2, 4
     X = _t(rng.random((n, d)), dev)
     w = _t(rng.standard_normal((P, n)), dev)
-    sm = mcmc.GPUSampler(X, w, _t(np.full(P, 3.0), dev), mcmc.ModelParams(d, P))
-    sm.run(2, np.random.default_rng(0), record=False)          # healthy
+    sm = mcmc.GPUSampler(X, w, _t(np.full(P, 3.0), dev), mcmc.ModelParams(d, P),
+                         use_graph=graph)
+    if not graph:
+        sm.run(2, np.random.default_rng(0), record=False)      # healthy
     prev = lib.gp_set_poll_budget(-1)
     try:
         with pytest.raises(kernels.FactorizationInternalError):
