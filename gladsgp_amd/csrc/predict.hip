@@ -137,6 +137,43 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
   }
 }
 
+// blockIdx.x -> (pair p, panel C).  Blocks b and b + 8 share an XCD (dispatch is round-robin
+// over the 8 XCDs), so with kXcdPanels = G > 0 the blocks of XCD slot x = b % 8 are laid out in
+// its own order t = b / 8 as groups of G panels (x, x + 8, ...) x all pairs, pair-major.  An
+// XCD's 64 resident blocks then hold G panels x 64/G pairs: each K* panel is read by 64/G
+// blocks at once and each L^-1 pair by G.  G = 0: pair-major over all panels (p = b / NC,
+// i.e. 16 panels x 4 pairs per XCD at C3, the K* panels re-fetched in every residency round).
+// C3 TRMM fabric traffic (FETCH_SIZE x2): G = 0 5.09 GB per launch, G = 4 4.52, G = 8 4.18;
+// launch time unchanged (profiles/r03/ab_map.log).  C4's 32 panels per GP give one group
+// either way.
+#ifndef TRMM_XCD_PANELS
+#define TRMM_XCD_PANELS 8
+#endif
+constexpr int kXcdPanels = TRMM_XCD_PANELS;
+GP_DEV void trmm_block_tile(int bid, int NI, int NC, int& p, int& C) {
+  const int NP = (NI + 1) / 2;
+  if (kXcdPanels > 0 && NC % (8 * kXcdPanels) == 0) {
+    const int x = bid & 7, t = bid >> 3, per = kXcdPanels * NP;
+    const int grp = t / per, j = t - grp * per;
+    p = j / kXcdPanels;
+    C = x + 8 * (grp * kXcdPanels + j % kXcdPanels);
+  } else {
+    p = bid / NC;
+    C = bid - p * NC;
+  }
+}
+
+// kDiagFirst: the second tile of a pair runs its diagonal block first.  A diagonal block's steps
+// carry few MFMAs (row tile r only meets L^-1 at steps t <= r) and are bound by the next
+// stage's load latency; with both tiles ending on their diagonal block every block of a
+// residency round spent its last 8 steps there together (all co-resident blocks at once), while
+// now pair p's two diagonal blocks sit back to back around step 8(NI - p), spread over the round.
+// Measured: C4 TRMM 2.059 -> 2.051 ms per launch, C3 unchanged (profiles/r03/ab_df.log).
+#ifndef TRMM_DIAG_FIRST
+#define TRMM_DIAG_FIRST 1
+#endif
+constexpr bool kDiagFirst = TRMM_DIAG_FIRST;
+
 // Row-tile pairs: block (p, C) computes tile (NI-1-p, C) and then tile (p, C), so every block
 // runs 8(NI+1) K steps (uniform work: at C3 the 512 blocks of a chunk are exactly one
 // residency wave of 2 per CU, no tail) and the second tile's first stage is fetched under the
@@ -148,7 +185,8 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
     int NI, int NC) {
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const int b = blockIdx.y;
-  const int p = blockIdx.x / NC, C = blockIdx.x % NC;
+  int p, C;
+  trmm_block_tile(blockIdx.x, NI, NC, p, C);
   const int Ihi = NI - 1 - p, Ilo = p;
   const int npass = (Ihi == Ilo) ? 1 : 2;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -187,22 +225,42 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
     const int s_diag = nsteps - BI / BK;
     int nst = nsteps;
     asm volatile("" : "+s"(nst));
-    int s = 0;
-    for (; s < s_diag; ++s) {
-      double* cur = smem + (s & 1) * STAGE;
-      if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
-      trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    for (; s < nsteps; ++s) {
-      double* cur = smem + (s & 1) * STAGE;
-      if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
-      else if (pass + 1 < npass) issue(Lb + Ilo * BI, 0, smem);   // next tile's first stage
-      const int t = s - s_diag;               // the wave's last row tile is 7 - wr
-      if (t <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, t);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    if (kDiagFirst && pass == 1) {
+      // the second tile: its diagonal block first (k-steps s_diag .., t = s), then k-steps 0 ..
+      for (int s = 0; s < BI / BK; ++s) {
+        double* cur = smem + (s & 1) * STAGE;
+        if (s + 1 < BI / BK) issue(L, s_diag + s + 1, smem + ((s + 1) & 1) * STAGE);
+        else if (nst > BI / BK) issue(L, 0, smem + ((s + 1) & 1) * STAGE);
+        if (s <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, s);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      for (int s = BI / BK; s < nsteps; ++s) {
+        double* cur = smem + (s & 1) * STAGE;
+        if (s + 1 < nst) issue(L, s + 1 - BI / BK, smem + ((s + 1) & 1) * STAGE);
+        trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    } else {
+      int s = 0;
+      for (; s < s_diag; ++s) {
+        double* cur = smem + (s & 1) * STAGE;
+        if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
+        trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      for (; s < nsteps; ++s) {
+        double* cur = smem + (s & 1) * STAGE;
+        if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
+        else if (pass + 1 < npass)               // next tile's first stage
+          issue(Lb + Ilo * BI, kDiagFirst ? Ilo * (BI / BK) : 0, smem);
+        const int t = s - s_diag;               // the wave's last row tile is 7 - wr
+        if (t <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
 
     // epilogue in stage buffer 1 (buffer 0 may hold the next tile's first stage)

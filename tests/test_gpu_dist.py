@@ -128,7 +128,7 @@ def _pipe_worker(rank, world, port, results):
     sys.path.insert(0, root)
     from gladsgp_amd import dist as gdist
     from gladsgp_amd import kernels
-    from gladsgp_amd.sharded import PipelinedPredictor, predict_sharded, split_counts
+    from gladsgp_amd.sharded import PipelinedPredictor, calibrate, predict_sharded, split_counts
     ctx = gdist.init_from_env("cuda", backend="gloo", device_index=0)
     out = {}
     try:
@@ -145,8 +145,14 @@ def _pipe_worker(rank, world, port, results):
         dd = torch.tensor([1e-6], dtype=torch.float64, device=dev)
         betas = [T(beta * (1.0 + 1e-3 * k)).reshape(1, d) for k in range(5)]
         gps = [(b, sd, dd, sd) for b in betas]
+        # the calibrated split (host-timed on a GPU both ranks share: at this small n the
+        # factorisation's host overhead alone can be worth every test point, so the pipeline
+        # below runs on a split that keeps rank 0 a share, to exercise its prediction too)
+        t_fact, t_point = calibrate(ctx, Xd, Xsd, betas[0], sd, dd, sd, yd)
+        out["calib"] = split_counts(m, world, t_fact / t_point)
+        counts = split_counts(m, world, min(t_fact / t_point, m / 4))
         # the package's two-stage pipeline over 5 GPs: GP k predicted while k+1 is factorised
-        pp = PipelinedPredictor(ctx, Xd, Xsd, yd, calib_gp=gps[0])
+        pp = PipelinedPredictor(ctx, Xd, Xsd, yd, counts=counts)
         pp.start(gps[0])
         res = [pp.step(gps[k + 1] if k + 1 < 5 else None) for k in range(5)]
         pp.finish()
@@ -225,6 +231,9 @@ def test_two_ranks_pipelined_and_sharded_single_gp():
         assert res["pipe"], res
         assert all(res["modes"].values()), res["modes"]
         assert res["raised"] == {"sharded": True, "pipeline": True}, res["raised"]
+    calib = results[0]["calib"]
+    assert calib == results[1]["calib"]                 # every rank computes the same split
+    assert sum(calib) == 40000 and len(calib) == 2 and 0 <= calib[0] <= calib[1]
     counts = results[0]["counts"]
     assert sum(counts) == 40000 and len(counts) == 2 and 0 < counts[0] <= counts[1]
 

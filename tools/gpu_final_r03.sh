@@ -45,7 +45,9 @@ tail -1 gpurun_out/${TAG}_latency.log | cut -c1-300
 step bench_n2
 timeout -k 10 400 python bench.py --gpus 2 --share-gpu --steps 5 --warmup 2 --no-cpu > gpurun_out/${TAG}_bench_n2.log 2>&1 || exit 1
 grep '^{' gpurun_out/${TAG}_bench_n2.log | cut -c1-300
+if [ -f _ab/libgpfit_r02.so ]; then
 step ab_r02
 timeout -k 10 200 python tools/ab_libs.py _ab/libgpfit_r02.so gladsgp_amd/libgpfit.so > gpurun_out/${TAG}_ab_r02.log 2>&1 || exit 1
 tail -4 gpurun_out/${TAG}_ab_r02.log
+fi
 step done
