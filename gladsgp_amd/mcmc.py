@@ -190,10 +190,17 @@ class GPUSampler:
     (n = 512, P = 8) 3.75 vs 4.04-4.26 ms per sweep eager, the fit 5.0-5.4 vs 5.7-6.3 s
     (profiles/r03/ab_mcmc_graph.log; round 2 measured the opposite while the factorisation
     still allocated its scratch inside every call).  Both paths run the same in-place sweep.
+
+    ``spec`` (default 2; GPFIT_MCMC_SPEC): likelihood-changing updates per batched gp_loglik,
+    evaluated speculatively for every outcome of the group's earlier updates (see _sweep).  At
+    n = 512 a factorisation is latency-bound (its 64-column chain), so evaluating 3P problems
+    costs about what P did: spec 2 takes a sweep from 11 gp_loglik calls to 6, 3.79 -> 2.86 ms
+    per sweep, the fit 5.05 -> 4.04 s; spec 3 (7P problems, worker-bound) 3.0 ms
+    (profiles/r03/ab_mcmc_spec.log).
     """
 
     def __init__(self, X: torch.Tensor, w_hat: torch.Tensor, LamSim: torch.Tensor,
-                 params: ModelParams, use_graph: bool | None = None):
+                 params: ModelParams, use_graph: bool | None = None, spec: int | None = None):
         self.X = X.contiguous()
         self.w = w_hat.contiguous()                 # (P, n)
         self.P, self.n = self.w.shape
@@ -215,6 +222,28 @@ class GPUSampler:
         self.use_graph = use_graph and self.dev.type == "cuda"
         self.graph = None
         self.st = None
+        if spec is None:
+            spec = int(os.environ.get("GPFIT_MCMC_SPEC", "2"))
+        if spec < 1:
+            raise ValueError("spec (updates per speculative group) must be >= 1")
+        # the likelihood-changing updates of a sweep, in mcmcList order (betaU row 0, the
+        # dummy x, moves under its prior alone)
+        ups = [("betaU", k) for k in range(1, self.d + 1)] + [(nm, None) for nm in
+                                                               ("lamUz", "lamWs", "lamWOs")]
+        self.groups = [ups[i:i + spec] for i in range(0, len(ups), spec)]
+        self.spec = spec
+        self._gbuf = {}
+        for g in self.groups:
+            sets = 2 ** len(g) - 1
+            if sets not in self._gbuf:
+                B = sets * self.P
+                self._gbuf[sets] = dict(
+                    ws=self.ws if B == self.P else kernels.LoglikWorkspace(self.n, B, self.dev),
+                    beta=torch.empty((B, self.d), dtype=F64, device=self.dev),
+                    s=torch.empty(B, dtype=F64, device=self.dev),
+                    delta=torch.empty(B, dtype=F64, device=self.dev),
+                    ll=torch.empty(B, dtype=F64, device=self.dev),
+                    w=self.w.repeat(sets, 1).contiguous())
 
     def _t(self, a) -> torch.Tensor:
         return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=self.dev)
@@ -275,10 +304,70 @@ class GPUSampler:
         return lp
 
     # -- one sweep -----------------------------------------------------------------------
+    def _fill(self, buf: dict, slot: int, st: dict) -> None:
+        """Model inputs (beta, s, delta) of the P GPs at parameter state ``st`` into rows
+        slot P .. (slot + 1) P of a speculative group's batch."""
+        sl = slice(slot * self.P, (slot + 1) * self.P)
+        buf["beta"][sl].copy_(st["betaU"][1:].transpose(0, 1))
+        torch.reciprocal(st["lamUz"], out=buf["s"][sl])
+        torch.add(torch.reciprocal(st["lamWs"]), torch.reciprocal(st["lamWOs"] * self.lam),
+                  out=buf["delta"][sl])
+
+    @staticmethod
+    def _with(st: dict, u, cand) -> dict:
+        """Parameter state ``st`` with update ``u``'s element(s) set to ``cand``."""
+        name, k = u
+        out = dict(st)
+        if name == "betaU":
+            b = st["betaU"].clone()
+            b[k] = cand
+            out["betaU"] = b
+        else:
+            out[name] = cand
+        return out
+
+    def _propose(self, u, take):
+        pr, st, steps, P = self.params, self.st, self.steps, self.P
+        name, k = u
+        p = getattr(pr, name)
+        if name == "betaU":
+            cur, step, m = st.betaU[k], steps["betaU"][k], P
+        elif name == "lamWOs":
+            cur, step, m = st.lamWOs, steps["lamWOs"].reshape(1), 1
+        else:
+            cur, step, m = getattr(st, name), steps[name].reshape(P), P
+        up, ua = take(m), take(m)
+        cand, ok = propose(p, cur, step, up)
+        return cand, ok, log_prior(p, cand) - log_prior(p, cur), ua, cur
+
+    def _accept(self, u, prop, ll_new) -> torch.Tensor:
+        """Metropolis decision for update ``u`` given the proposal's per-GP likelihood."""
+        st = self.st
+        cand, ok, dlp, ua, cur = prop
+        name, k = u
+        if name == "lamWOs":                 # shared by every GP: accepted on the sum
+            acc = ok & (torch.log(ua) < (ll_new - st.ll).sum() + dlp.sum())
+        else:
+            acc = ok & (torch.log(ua) < ll_new - st.ll + dlp)
+        cur.copy_(torch.where(acc, cand, cur))
+        st.ll.copy_(torch.where(acc, ll_new, st.ll))
+        st.acc[("betaU", k) if name == "betaU" else name].add_(acc.to(F64))
+        return acc
+
     def _sweep(self) -> None:
         """One component-wise Metropolis sweep on the static buffers (graph-capturable: no
-        allocation that outlives it, no host synchronisation, in-place state updates)."""
-        pr, st, P, d, u, steps = self.params, self.st, self.P, self.d, self.u, self.steps
+        allocation that outlives it, no host synchronisation, in-place state updates).
+
+        Speculative groups: the updates u_1 .. u_g of a group are proposed together and ONE
+        batched gp_loglik evaluates, for every i, u_i's proposal at each of the 2^(i-1)
+        accept/reject outcomes of u_1 .. u_i-1 (2^g - 1 parameter states x P GPs); the
+        decisions are then taken in order, each reading the likelihood of the outcome that
+        actually happened (per GP: the P GPs are independent given lamWOs, whose decision is
+        one for all).  Proposals, uniforms and decisions are those of the one-update-at-a-time
+        sweep, so the chain is the same Markov chain, draw for draw; what changes is that the
+        factorisations, whose latency (a 64-column chain step per tile) bounds a sweep at
+        n = 512, are issued g at a time (spec = 1: one call per update)."""
+        pr, st, P, u = self.params, self.st, self.P, self.u
         o = 0
 
         def take(k):
@@ -287,46 +376,33 @@ class GPUSampler:
             o += k
             return r
 
-        # betaU, one row (all P GPs) at a time
-        for k in range(d + 1):
-            up, ua = take(P), take(P)
-            cur = st.betaU[k]
-            cand, ok = propose(pr.betaU, cur, steps["betaU"][k], up)
-            dlp = log_prior(pr.betaU, cand) - log_prior(pr.betaU, cur)
-            if k == 0:                       # dummy x: the likelihood does not depend on it
-                acc = ok & (torch.log(ua) < dlp)
-            else:
-                trial = st.betaU.clone()
-                trial[k] = cand
-                ll_new = self.loglik(trial, st.lamUz, st.lamWs, st.lamWOs)
-                acc = ok & (torch.log(ua) < ll_new - st.ll + dlp)
-                st.ll.copy_(torch.where(acc, ll_new, st.ll))
-            st.betaU[k].copy_(torch.where(acc, cand, cur))
-            st.acc[("betaU", k)].add_(acc.to(F64))
-        # lamUz, lamWs: all P GPs at once
-        for name in ("lamUz", "lamWs"):
-            up, ua = take(P), take(P)
-            cur = getattr(st, name)
-            p = getattr(pr, name)
-            cand, ok = propose(p, cur, steps[name].reshape(P), up)
-            args = {"lamUz": st.lamUz, "lamWs": st.lamWs}
-            args[name] = cand
-            ll_new = self.loglik(st.betaU, args["lamUz"], args["lamWs"], st.lamWOs)
-            acc = ok & (torch.log(ua) < ll_new - st.ll + log_prior(p, cand) - log_prior(p, cur))
-            cur.copy_(torch.where(acc, cand, cur))
-            st.ll.copy_(torch.where(acc, ll_new, st.ll))
-            st.acc[name].add_(acc.to(F64))
-        # lamWOs: shared by every GP, accepted on the sum
-        up, ua = take(1), take(1)
-        p = pr.lamWOs
-        cur = st.lamWOs
-        cand, ok = propose(p, cur, steps["lamWOs"].reshape(1), up)
-        ll_new = self.loglik(st.betaU, st.lamUz, st.lamWs, cand)
-        dl = (ll_new - st.ll).sum() + (log_prior(p, cand) - log_prior(p, cur)).sum()
-        acc = ok & (torch.log(ua) < dl)
+        # betaU row 0 (the dummy x): the likelihood does not depend on it
+        cand, ok, dlp, ua, cur = self._propose(("betaU", 0), take)
+        acc = ok & (torch.log(ua) < dlp)
         cur.copy_(torch.where(acc, cand, cur))
-        st.ll.copy_(torch.where(acc, ll_new, st.ll))
-        st.acc["lamWOs"].add_(acc.to(F64))
+        st.acc[("betaU", 0)].add_(acc.to(F64))
+        for grp in self.groups:
+            props = [self._propose(g, take) for g in grp]
+            buf = self._gbuf[2 ** len(grp) - 1]
+            s0 = {"betaU": st.betaU, "lamUz": st.lamUz, "lamWs": st.lamWs, "lamWOs": st.lamWOs}
+            slot, base = 0, []
+            for i, g in enumerate(grp):
+                base.append(slot)
+                for pat in range(2 ** i):         # outcome pattern of the group's earlier updates
+                    sx = s0
+                    for j in range(i):
+                        if (pat >> j) & 1:
+                            sx = self._with(sx, grp[j], props[j][0])
+                    self._fill(buf, slot, self._with(sx, g, props[i][0]))
+                    slot += 1
+            ll_all = kernels.loglik(self.X, buf["beta"], buf["s"], buf["delta"], buf["w"],
+                                    buf["ws"], out=buf["ll"]).view(-1, P)
+            pat = None
+            for i, g in enumerate(grp):
+                ll_i = ll_all[base[i]:base[i] + 2 ** i]
+                ll_new = ll_i[0] if pat is None else ll_i.gather(0, pat.view(1, P)).view(P)
+                acc = self._accept(g, props[i], ll_new).expand(P).long() << i
+                pat = acc if pat is None else pat + acc
         self.lp.copy_(self.log_post().reshape(1))
 
     def _capture(self) -> None:
@@ -372,7 +448,8 @@ class GPUSampler:
                     rec["logPost"][i].copy_(self.lp)
         # one host check per run: a factorisation that gave up (info = -1) would otherwise be a
         # silently rejected proposal (ll = NaN); a non-PD proposal (ll = -inf) is a rejection
-        self.ws.check_status()
+        for ws in {id(w): w for w in [self.ws] + [b["ws"] for b in self._gbuf.values()]}.values():
+            ws.check_status()
         return {k: v.cpu().numpy() for k, v in rec.items()} if record else None
 
 

@@ -71,15 +71,21 @@ def _spec(pr):
                 getattr(pr, k).mcmcStepType) for k in pr.names}
 
 
-@pytest.mark.parametrize("n,d,P,steps_scale,graph", [(48, 2, 3, 1.0, False),
-                                                     (48, 2, 3, 1.0, True),
-                                                     (130, 3, 2, 0.3, True)])
-def test_chain_matches_oracle(dev, n, d, P, steps_scale, graph):
+@pytest.mark.parametrize("n,d,P,steps_scale,graph,spec", [(48, 2, 3, 1.0, False, 1),
+                                                          (48, 2, 3, 1.0, True, 1),
+                                                          (48, 2, 3, 1.0, False, 2),
+                                                          (48, 2, 3, 1.0, True, 3),
+                                                          (130, 3, 2, 0.3, True, 2),
+                                                          (130, 3, 2, 0.3, False, 3)])
+def test_chain_matches_oracle(dev, n, d, P, steps_scale, graph, spec):
+    """The oracle runs one update at a time; the sampler's speculative groups (spec updates per
+    batched gp_loglik, 2^spec - 1 parameter states) must give the same chain."""
     X, w, lam = _problem(n, d, P, seed=11 + n)
     pr = mcmc.ModelParams(d, P)
     for k in pr.names:
         getattr(pr, k).mcmcStepParam = getattr(pr, k).mcmcStepParam * steps_scale
-    sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr, use_graph=graph)
+    sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr, use_graph=graph,
+                              spec=spec)
     nsw = 25
     rec = sampler.run(nsw, np.random.default_rng(5))
     U = np.random.default_rng(5).random((nsw, mcmc.uniforms_per_sweep(d, P)))
@@ -138,3 +144,18 @@ def test_fit_models_roundtrip(dev, tmp_path):
     pred = SepiaEmulatorPrediction(model=mdl, samples=samples, t_pred=rng.random((7, d)))
     assert pred.w.shape == (4, 7, 3) and np.all(np.isfinite(pred.var))
     assert pred.get_y().shape == (4, 7, ny)
+
+
+def test_speculative_groups_same_chain(dev):
+    """spec = 1 .. 4 (up to 15 parameter states x P GPs per gp_loglik) give the same chain: the
+    batch a likelihood is evaluated in does not change its value."""
+    n, d, P = 96, 3, 4
+    X, w, lam = _problem(n, d, P, seed=31)
+    recs = []
+    for spec in (1, 2, 3, 4):
+        pr = mcmc.ModelParams(d, P)
+        sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr, spec=spec)
+        recs.append(sampler.run(30, np.random.default_rng(9)))
+    for r in recs[1:]:
+        for k in ("betaU", "lamUz", "lamWs", "lamWOs", "logPost"):
+            np.testing.assert_allclose(r[k], recs[0][k], rtol=1e-12, atol=1e-12, err_msg=k)
