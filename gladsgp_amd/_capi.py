@@ -75,6 +75,9 @@ SIGNATURES = {
                           c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,
                           c_void_p]),
     "gp_loglik_status": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "gp_mcmc_group_prep": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+    "gp_mcmc_group_decide": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "gp_realize": (c_int, [c_void_p, c_void_p, c_ll, ctypes.c_ulonglong, ctypes.c_ulonglong,
                            c_void_p, c_void_p]),
     "gp_dgemm_ws_bytes": (c_ll, [c_int, c_int, c_int]),
@@ -161,3 +164,18 @@ def call(name: str, *args) -> int:
 
 def exported_symbols() -> list[str]:
     return list(SIGNATURES)
+
+
+MCMC_MAX_GROUP = 4            # GPFIT_MCMC_MAX_GROUP
+MCMC_DIST = {"Gamma": 0, "Beta": 1, "Normal": 2, "Uniform": 3}
+MCMC_STEP = {"Uniform": 0, "BetaRho": 1}
+
+
+class McmcState(ctypes.Structure):
+    """gp_mcmc_state (include/gpfit.h): the sampler's device buffers and priors."""
+    _fields_ = [(nm, c_void_p) for nm in (
+        "betaU", "lamUz", "lamWs", "lamWOs", "ll", "lam", "u", "step_betaU", "step_lamUz",
+        "step_lamWs", "step_lamWOs", "acc", "lp", "scratch")] + [
+        ("P", c_int), ("d", c_int), ("dist", c_int * 4), ("steptype", c_int * 4),
+        ("pa", ctypes.c_double * 4), ("pb", ctypes.c_double * 4), ("lo", ctypes.c_double * 4),
+        ("hi", ctypes.c_double * 4)]

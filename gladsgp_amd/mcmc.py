@@ -63,6 +63,7 @@ width for a bounded parameter.  Burn-in, ladder base, target, regularisation and
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from dataclasses import dataclass, field
@@ -70,7 +71,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from . import kernels
+from . import _capi, kernels
 
 F64 = torch.float64
 TARGET_LOGIT = math.log(1.0 / (math.e - 1.0))   # acceptance 1/e
@@ -200,7 +201,8 @@ class GPUSampler:
     """
 
     def __init__(self, X: torch.Tensor, w_hat: torch.Tensor, LamSim: torch.Tensor,
-                 params: ModelParams, use_graph: bool | None = None, spec: int | None = None):
+                 params: ModelParams, use_graph: bool | None = None, spec: int | None = None,
+                 fused: bool | None = None):
         self.X = X.contiguous()
         self.w = w_hat.contiguous()                 # (P, n)
         self.P, self.n = self.w.shape
@@ -232,6 +234,13 @@ class GPUSampler:
                                                                ("lamUz", "lamWs", "lamWOs")]
         self.groups = [ups[i:i + spec] for i in range(0, len(ups), spec)]
         self.spec = spec
+        if fused is None:
+            fused = os.environ.get("GPFIT_MCMC_FUSED", "1") == "1"
+        self.fused = fused and self.dev.type == "cuda"
+        if self.fused and spec > _capi.MCMC_MAX_GROUP:
+            raise ValueError(f"spec > {_capi.MCMC_MAX_GROUP} needs fused=False")
+        self._S = None
+        self._scratch = torch.zeros(3 * _capi.MCMC_MAX_GROUP * self.P, dtype=F64, device=self.dev)
         self._gbuf = {}
         for g in self.groups:
             sets = 2 ** len(g) - 1
@@ -257,9 +266,12 @@ class GPUSampler:
         if self.st is None:
             z = torch.zeros(self.P, dtype=F64, device=self.dev)
             self.st = ChainState(*[v.clone() for v in vals], z.clone())
-            self.st.acc = {("betaU", k): z.clone() for k in range(self.d + 1)}
-            self.st.acc.update({"lamUz": z.clone(), "lamWs": z.clone(),
-                                "lamWOs": torch.zeros(1, dtype=F64, device=self.dev)})
+            # one (d + 4, P) block indexed by update code (gp_mcmc_state.acc), viewed per update
+            d = self.d
+            self._acc = torch.zeros((d + 4, self.P), dtype=F64, device=self.dev)
+            self.st.acc = {("betaU", k): self._acc[k] for k in range(d + 1)}
+            self.st.acc.update({"lamUz": self._acc[d + 1], "lamWs": self._acc[d + 2],
+                                "lamWOs": self._acc[d + 3, :1]})
         else:
             for t, v in zip((self.st.betaU, self.st.lamUz, self.st.lamWs, self.st.lamWOs),
                             vals):
@@ -354,9 +366,60 @@ class GPUSampler:
         st.acc[("betaU", k) if name == "betaU" else name].add_(acc.to(F64))
         return acc
 
+    def _code(self, u) -> int:
+        name, k = u
+        return k if name == "betaU" else self.d + {"lamUz": 1, "lamWs": 2, "lamWOs": 3}[name]
+
+    def _state_struct(self) -> "_capi.McmcState":
+        """gp_mcmc_state over the static buffers and the current priors."""
+        st, pr = self.st, self.params
+        S = _capi.McmcState()
+        for nm, t in (("betaU", st.betaU), ("lamUz", st.lamUz), ("lamWs", st.lamWs),
+                      ("lamWOs", st.lamWOs), ("ll", st.ll), ("lam", self.lam), ("u", self.u),
+                      ("step_betaU", self.steps["betaU"]), ("step_lamUz", self.steps["lamUz"]),
+                      ("step_lamWs", self.steps["lamWs"]), ("step_lamWOs", self.steps["lamWOs"]),
+                      ("acc", self._acc), ("lp", self.lp), ("scratch", self._scratch)):
+            if not t.is_contiguous() or t.dtype != F64:
+                raise TypeError(f"mcmc state buffer {nm} must be contiguous float64")
+            setattr(S, nm, t.data_ptr())
+        S.P, S.d = self.P, self.d
+        for i, nm in enumerate(ModelParams.names):
+            p = getattr(pr, nm)
+            S.dist[i] = _capi.MCMC_DIST[p.dist]
+            S.steptype[i] = _capi.MCMC_STEP[p.mcmcStepType]
+            S.pa[i], S.pb[i] = p.params
+            S.lo[i], S.hi[i] = p.bounds
+        return S
+
     def _sweep(self) -> None:
+        if self.fused:
+            self._sweep_fused()
+        else:
+            self._sweep_torch()
+
+    def _sweep_fused(self) -> None:
+        """The sweep of _sweep_torch with each speculative group's proposals and decisions in
+        two single-workgroup kernels around its gp_loglik (gp_mcmc_group_prep / _decide,
+        csrc/mcmc.hip): 3 launches + gp_loglik's per group instead of ~100."""
+        self._S = self._state_struct()          # kept alive: the library reads it per call
+        stream = kernels._stream(self.dev)
+        last = len(self.groups) - 1
+        for gi, grp in enumerate(self.groups):
+            buf = self._gbuf[2 ** len(grp) - 1]
+            kinds = (ctypes.c_int * len(grp))(*[self._code(g) for g in grp])
+            _capi.call("gp_mcmc_group_prep", ctypes.addressof(self._S), ctypes.addressof(kinds),
+                       len(grp), int(gi == 0), buf["beta"].data_ptr(), buf["s"].data_ptr(),
+                       buf["delta"].data_ptr(), stream)
+            kernels.loglik(self.X, buf["beta"], buf["s"], buf["delta"], buf["w"], buf["ws"],
+                           out=buf["ll"])
+            _capi.call("gp_mcmc_group_decide", ctypes.addressof(self._S),
+                       ctypes.addressof(kinds), len(grp), int(gi == last), buf["ll"].data_ptr(),
+                       stream)
+
+    def _sweep_torch(self) -> None:
         """One component-wise Metropolis sweep on the static buffers (graph-capturable: no
-        allocation that outlives it, no host synchronisation, in-place state updates).
+        allocation that outlives it, no host synchronisation, in-place state updates), as
+        tensor ops (the host-logic reference of the fused sweep; runs on any device).
 
         Speculative groups: the updates u_1 .. u_g of a group are proposed together and ONE
         batched gp_loglik evaluates, for every i, u_i's proposal at each of the 2^(i-1)

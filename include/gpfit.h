@@ -251,6 +251,58 @@ int gp_loglik(const double* X, int n, int d, int ldx, const double* beta, int ld
 int gp_loglik_status(void* ws, int n, int batch, int reset, hipStream_t stream);
 
 /*
+ * Metropolis sweep steps around gp_loglik (the GPU sampler's speculative groups; replaces the
+ * proposal / accept logic of SEPIA's SepiaModel.do_mcmc / tune_step_sizes that src/model.py:
+ * 225-235 drives).  The chain state and its priors are described by a gp_mcmc_state of device
+ * pointers (row-major: betaU and step_betaU (d+1) x P; lamUz, lamWs, ll, lam, step_lamUz,
+ * step_lamWs P; lamWOs, step_lamWOs 1; acc (d+4) x P acceptance counters indexed by update
+ * code; u the sweep's 2 ((d+1) P + 2 P + 1) uniforms, an update's proposal uniforms then its
+ * acceptance uniforms, in update order; scratch 3 * GPFIT_MCMC_MAX_GROUP * P doubles) plus the
+ * prior family / parameters / bounds and step type of each of betaU, lamUz, lamWs, lamWOs.
+ * Update codes: 1..d betaU row, d+1 lamUz, d+2 lamWs, d+3 lamWOs.  For a group of g updates:
+ *   gp_mcmc_group_prep   proposes them (first != 0: also the prior-only move of betaU row 0)
+ *                        and writes the Gram inputs of the 2^g - 1 state sets, set
+ *                        2^i - 1 + pat = update i proposed after the outcomes `pat` (bit q =
+ *                        update q accepted) of updates 0..i-1, rows set * P + j of beta
+ *                        (x d), s and delta: the batch for gp_loglik;
+ *   gp_mcmc_group_decide takes the decisions in order from gp_loglik's ll_all (per GP; lamWOs
+ *                        once on the sum), updates state, ll and counters in place and
+ *                        (last != 0) writes the log posterior to lp.
+ * Single-workgroup launches (P <= 1024), stream-ordered, graph-capturable; 0 or < 0 (argument).
+ */
+#define GPFIT_MCMC_MAX_GROUP 4
+#define GPFIT_MCMC_GAMMA 0        /* (a - 1) log x - b x                                      */
+#define GPFIT_MCMC_BETA 1         /* Beta(a, b) on rho = min(exp(-x / 4), 0.999)              */
+#define GPFIT_MCMC_NORMAL 2       /* -1/2 ((x - a) / b)^2                                     */
+#define GPFIT_MCMC_UNIFORM 3      /* 0 (the bounds)                                           */
+#define GPFIT_MCMC_STEP_UNIFORM 0 /* x' = x + step (u - 1/2)                                  */
+#define GPFIT_MCMC_STEP_BETARHO 1 /* the same move on rho = exp(-x / 4)                       */
+typedef struct {
+  double* betaU;
+  double* lamUz;
+  double* lamWs;
+  double* lamWOs;
+  double* ll;
+  const double* lam;
+  const double* u;
+  const double* step_betaU;
+  const double* step_lamUz;
+  const double* step_lamWs;
+  const double* step_lamWOs;
+  double* acc;
+  double* lp;
+  double* scratch;
+  int P, d;
+  int dist[4];        /* per parameter: betaU, lamUz, lamWs, lamWOs */
+  int steptype[4];
+  double pa[4], pb[4], lo[4], hi[4];
+} gp_mcmc_state;
+int gp_mcmc_group_prep(const gp_mcmc_state* S, const int* kinds, int g, int first,
+                       double* beta, double* s, double* delta, hipStream_t stream);
+int gp_mcmc_group_decide(const gp_mcmc_state* S, const int* kinds, int g, int last,
+                         const double* ll_all, hipStream_t stream);
+
+/*
  * One marginal realisation per entry: out[i] = mean[i] + sqrt(max(var[i], 0)) z_i, z_i ~ N(0,1)
  * from counter-based Philox4x32-10 keyed by `seed` (counter (i/2, offset); Box-Muller pairs),
  * so the draws depend only on (seed, offset, i).  out may alias mean.  The opt-in realize mode

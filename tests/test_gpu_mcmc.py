@@ -159,3 +159,24 @@ def test_speculative_groups_same_chain(dev):
     for r in recs[1:]:
         for k in ("betaU", "lamUz", "lamWs", "lamWOs", "logPost"):
             np.testing.assert_allclose(r[k], recs[0][k], rtol=1e-12, atol=1e-12, err_msg=k)
+
+
+@pytest.mark.parametrize("spec,graph", [(1, False), (2, True), (4, False)])
+def test_fused_sweep_equals_tensor_sweep(dev, spec, graph):
+    """gp_mcmc_group_prep / _decide (csrc/mcmc.hip) against the tensor-op sweep they replace:
+    the same proposals, decisions and counters (op-for-op arithmetic, no FMA contraction)."""
+    n, d, P = 72, 4, 5
+    X, w, lam = _problem(n, d, P, seed=41)
+    recs, cnts = [], []
+    for fused in (False, True):
+        pr = mcmc.ModelParams(d, P)
+        sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr, use_graph=graph,
+                                  spec=spec, fused=fused)
+        assert sampler.fused == fused
+        recs.append(sampler.run(30, np.random.default_rng(13)))
+        cnts.append(sampler.counts())
+    for k in ("betaU", "lamUz", "lamWs", "lamWOs"):
+        np.testing.assert_array_equal(recs[1][k], recs[0][k], err_msg=k)
+    np.testing.assert_allclose(recs[1]["logPost"], recs[0]["logPost"], rtol=1e-13, atol=0)
+    for k in cnts[0]:
+        np.testing.assert_array_equal(cnts[1][k], cnts[0][k], err_msg=str(k))
