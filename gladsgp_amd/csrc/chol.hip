@@ -349,7 +349,8 @@ __device__ __attribute__((noinline)) int diag_factor_inv(int nb, double* ld_out)
 //                  L_rb = A_rb Dinv_b^T (r > b)     waves 1-3, one MFMA block each
 //                  A_rs -= L_rb L_sb^T (b < s <= r) wave 0 takes (b+1, b+1) and goes straight on
 //                                                   to the next leaf; waves 1-3 the rest
-//   X_rc = -Dinv_r sum_{k=c}^{r-1} L_rk X_kc        wave c builds column block c of L^-1
+//   X_rc = -Dinv_r sum_{k=c}^{r-1} L_rk X_kc        row r of L^-1 by waves 1-2 beside leaf r+1,
+//                                                   the last row by waves 0-2 after leaf 3
 // The leaf is the 16-column symmetric elimination of diag_factor_inv held in ONE wave's
 // registers (lanes 0-15 = columns of A, lanes 16-31 = columns of I for the inverse, same row
 // operations), the broadcasts are readlanes instead of LDS round trips, and every block
@@ -444,9 +445,26 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
   lds_double* U = sm.Bs;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   lds_double* piv = sm.invs;
+  // X_rc = -Dinv_r sum_{k=c}^{r-1} L_rk X_kc (X_cc = Dinv_c) into U's block (r, c); the sum
+  // passes through T's free upper block (c, r)
+  auto inv_block = [&](int r, int c) {
+    f64x4 acc = zero4();
+    for (int k = c; k < r; ++k)
+      mm16(acc, T + 16 * r * LP + 16 * k, LP, 1, U + 16 * k * LP + 16 * c, LP, 1, false);
+    lds_double* tmp = T + 16 * c * LP + 16 * r;
+    st16(tmp, acc, 1.0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the block is in LDS before it is read
+    f64x4 x = zero4();
+    mm16(x, U + 16 * r * LP + 16 * r, LP, 1, tmp, LP, 1, false);
+    st16(U + 16 * r * LP + 16 * c, x, -1.0);
+  };
   static_for<0, 4, 1>([&](auto Bk) {
     constexpr int b = decltype(Bk)::value;
+    // while wave 0 factors leaf b, waves 1-2 build row b-1 of the inverse (its inputs -- Dinv of
+    // rows <= b-1, the final L_{b-1,k}, the rows above -- are all complete), which the serial
+    // phase after the last leaf used to do
     if (w == 0) leaf16(T, U, 16 * b, piv);
+    else if (b >= 2 && w <= b - 1) inv_block(b - 1, w - 1);
     __syncthreads();
     if constexpr (b < 3) {
       // panel: L_rb = A_rb Dinv_b^T, r = b + w
@@ -473,8 +491,8 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
         }
     }
   });
-  // inverse: wave c builds column block c (X_cc = Dinv_c already in U); scratch = T's upper
-  // block (c, r).  Wave 3 meanwhile checks the 64 pivots and sums their logs.
+  // the inverse's last row: wave c builds X_3c (rows 1 and 2 were built beside leaves 2 and 3;
+  // X_cc = Dinv_c already in U).  Wave 3 meanwhile checks the 64 pivots and sums their logs.
   if (w == 3) {
     const int lane = threadIdx.x & 63;
     const double p = piv[lane];
@@ -488,20 +506,7 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
       sm.red[0] = l;
     }
   }
-  if (w < 3) {
-    const int c = w;
-    for (int r = c + 1; r <= 3; ++r) {
-      f64x4 acc = zero4();
-      for (int k = c; k < r; ++k)
-        mm16(acc, T + 16 * r * LP + 16 * k, LP, 1, U + 16 * k * LP + 16 * c, LP, 1, false);
-      lds_double* tmp = T + 16 * c * LP + 16 * r;
-      st16(tmp, acc, 1.0);
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the block is in LDS before it is read
-      f64x4 x = zero4();
-      mm16(x, U + 16 * r * LP + 16 * r, LP, 1, tmp, LP, 1, false);
-      st16(U + 16 * r * LP + 16 * c, x, -1.0);
-    }
-  }
+  if (w < 3) inv_block(3, w);   // the last row of the inverse (rows 1, 2: beside the leaves)
   __syncthreads();
   // zero the strict upper blocks of L^-1 (the chain's GEMM and the D_j store read the whole
   // tile; L's upper blocks are never read: it is stored lower-only, then overwritten)

@@ -51,3 +51,7 @@ timeout -k 10 200 python tools/ab_libs.py _ab/libgpfit_r02.so gladsgp_amd/libgpf
 tail -4 gpurun_out/${TAG}_ab_r02.log
 fi
 step done
+step ab_spec
+bash tools/ab_mcmc_spec.sh ${TAG}_ab_spec 2 3 > /dev/null || exit 1
+cat gpurun_out/${TAG}_ab_spec.log
+step end
