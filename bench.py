@@ -486,6 +486,9 @@ def main():
     print(json.dumps(line), flush=True)
 
 
+C4_DEFAULT_CHUNK = 8192   # the library's default test-point chunk for a batch (predict.hip)
+
+
 def main_c4(args):
     from gladsgp_amd.emulator import assemble_units
     ctx = gdist.init_from_env("cuda")
@@ -551,9 +554,10 @@ def main_c4(args):
     tr_flops = float(bl) * m * K * (n * n + 4 * n)
     traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_c4.json")
-    if os.path.exists(tf) and ctx.world == 1 and args.m_chunk in (0, 4096):
+    if os.path.exists(tf) and ctx.world == 1:
         tj = json.load(open(tf))
-        if tj.get("n") == n and tj.get("batch") == P and tj.get("m") == m:
+        if (tj.get("n") == n and tj.get("batch") == P and tj.get("m") == m and
+                tj.get("m_chunk") == (args.m_chunk or C4_DEFAULT_CHUNK)):
             traffic = tj["kernels"]["trmm_pair_kernel"]["bytes_per_launch"]
             traffic_src = "profiles/r03/pmc_traffic_c4.json (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
     tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12 if tr_ms > 0 else 0.0

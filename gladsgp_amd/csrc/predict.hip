@@ -31,7 +31,7 @@ constexpr int BI = 128;   // V tile rows (L^-1 rows)
 constexpr int BC = 128;   // V tile cols (test points)
 constexpr int BK = 16;    // K step
 constexpr long long kDefaultChunkElems = 256ll << 20;  // <= 2 GB of Kt per chunk
-constexpr int kDefaultChunk = 4096;                   // test points per chunk (batches)
+constexpr int kDefaultChunk = 8192;                   // test points per chunk (batches)
 constexpr int kDefaultChunkSingle = 16384;            // ... and for one GP
 
 // Cross-covariance chunk, k-major as the TRMM streams it:
@@ -144,8 +144,7 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
 // blocks at once and each L^-1 pair by G.  G = 0: pair-major over all panels (p = b / NC,
 // i.e. 16 panels x 4 pairs per XCD at C3, the K* panels re-fetched in every residency round).
 // C3 TRMM fabric traffic (FETCH_SIZE x2): G = 0 5.09 GB per launch, G = 4 4.52, G = 8 4.18;
-// launch time unchanged (profiles/r03/ab_map.log).  C4's 32 panels per GP give one group
-// either way.
+// launch time unchanged (profiles/r03/ab_map.log).
 #ifndef TRMM_XCD_PANELS
 #define TRMM_XCD_PANELS 8
 #endif
@@ -434,8 +433,10 @@ Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false,
   if (m_chunk > 0) {
     mc = gp_ceil_div(m_chunk, BC) * BC;
   } else {
-    // Test points per chunk: 4096 measured best for batches (C4, tools/job_c4chunk.sh) and
-    // 16384 for one GP (C3 with the row-pair TRMM: a launch is then 2048 blocks, four full
+    // Test points per chunk: 8192 for batches (C4: 64 panels per GP, so the TRMM's XCD-aware
+    // order applies; 60.2-62.1 vs 62.6-63.0 ms per step at 4096 in three same-box rounds,
+    // profiles/r03/sweep_c4_chunk_r03.log -- round 1 had measured 4096 best with the plain
+    // order) and 16384 for one GP (C3 with the row-pair TRMM: a launch is then 2048 blocks, four full
     // residency waves; 28.51-28.59 vs 28.72-28.81 ms per step at 4096, 32768 slower:
     // profiles/r01/sweep_c3_chunk_pair.log).  Shrunk only when the batch's cross-covariance
     // slab would exceed kDefaultChunkElems doubles.

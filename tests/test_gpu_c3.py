@@ -4,7 +4,7 @@ The oracle (numpy fp64) runs at the full n = 4096 on a 2000-point sample of the 
 whole 100k-point prediction is checked through size-independent properties:
   * oracle agreement on the sample: max|dmean| <= 1e-8 max|mean|, max|dvar| <= 1e-8 s (SURVEY
     §8c's C3 tolerance; kappa(G) ~ 1e8 at the 1e-6 jitter);
-  * chunk invariance: the default 4096-point chunks and 1280-point chunks give bit-identical
+  * chunk invariance: the default 16384-point chunks and 1280-point chunks give bit-identical
     answers (chunk edges are multiples of the 128-point tile, so every test point is reduced by
     the same tiles in the same order);
   * prefix invariance: predicting only the first 2000 points reproduces those entries exactly;

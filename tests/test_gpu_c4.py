@@ -6,7 +6,7 @@ beta_j = rng(10 + j), w_j = rng(100 + j), X* = rng(2), s = 1, delta = 1e-6).
   gp_fit_predict on a context — against the numpy oracle for PCs 0, 9, 22, 31 on a 2000-point
   sample: max|dmean| <= 1e-8 max|mean|, max|dvar| <= 1e-8 s (SURVEY §8c, kappa-limited);
 * the two paths agree bit for bit over all 32 x 100k predictions;
-* chunk invariance (1280-point vs the default 4096-point chunks) and prefix invariance: bit
+* chunk invariance (1280-point vs the default 8192-point chunks) and prefix invariance: bit
   identical; bounds 0 <= var <= s;
 * the 8-way round-robin PC deal of the sharded run (4 PCs per rank, as on 8 GPUs) predicted
   rank by rank and reassembled by emulator.unit_order equals the unsharded batch bit for bit.

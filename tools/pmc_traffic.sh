@@ -29,8 +29,8 @@ t = means.get("trmm_pair_kernel", {})
 if t:
     if WL == "c3":
         n, m, chunk, batch, launches = 4096, 100000, 16384, 1, 7
-    else:                                # C4: 32 GPs, n = 1024, 4096-point chunks
-        n, m, chunk, batch, launches = 1024, 100000, 4096, 32, 25
+    else:                                # C4: 32 GPs, n = 1024, 8192-point chunks
+        n, m, chunk, batch, launches = 1024, 100000, 8192, 32, 13
     L = 8.0 * n * (n + 1) / 2 * batch    # L^-1 lower triangles
     kt = 8.0 * n * m / launches * batch  # mean Kt chunk per launch
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of "
