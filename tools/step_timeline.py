@@ -36,3 +36,20 @@ gap = 0
 for a, b in zip(tr, tr[1:]):
     gap += max(0, int(b["Start_Timestamp"]) - int(a["End_Timestamp"]))
 print(f"  prediction phase: {len(tr)} kernels, idle between them {gap / 1e3:.1f} us")
+# the step period (Gram to Gram) and what runs between the last prediction kernel of one step
+# and the Gram of the next
+if len(starts) > 2:
+    per = [(int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
+           for a, b in zip(starts, starts[1:])]
+    print(f"  step period (Gram to Gram) us: min {min(per):.1f} median "
+          f"{sorted(per)[len(per) // 2]:.1f} max {max(per):.1f} over {len(per)}")
+    last_pred = max(int(r["End_Timestamp"]) for r in tr)
+    nxt = rows[starts[-1]]
+    print(f"  last prediction kernel end -> next Gram start: "
+          f"{(int(nxt['Start_Timestamp']) - last_pred) / 1e3:.1f} us; between them:")
+    for r in rows:
+        s0 = int(r["Start_Timestamp"])
+        if last_pred - 50000 <= s0 <= int(nxt["Start_Timestamp"]) and name(r) not in (
+                "trmm_pair_kernel", "finalize_kernel"):
+            print(f"    {name(r):28s} start {(s0 - last_pred) / 1e3:8.1f} us  dur "
+                  f"{(int(r['End_Timestamp']) - s0) / 1e3:7.1f} us")
