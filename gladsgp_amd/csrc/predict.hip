@@ -703,10 +703,14 @@ namespace {
 // CUs at once doubled the early, bandwidth-bound trailing updates, so it ran CU-masked from 40%
 // of the block steps (profiles/r01/ab_cross_select_exp.log).  With the persistent
 // factorisation (1.9 ms, the cross-covariance's start event recorded before its launch) and
-// per-chunk events, leaving 32 CUs free is best: 27.03-27.11 ms/step vs 27.03-27.14 for no
+// per-chunk events, leaving 32 CUs free was best: 27.03-27.11 ms/step vs 27.03-27.14 for no
 // mask, 27.31-27.57 for 64-96 and 27.79-27.88 for 128 (profiles/r02/sweep_cross_mask_r02e.log).
+// Round 3's factorisation (1.82 ms alone) loses little to an unmasked cross-covariance, which
+// then ends 0.3 ms sooner, before the first TRMM launch needs the GPU: no mask 26.68-26.71
+// ms/step vs 26.87-26.95 for 32 CUs, 27.08-27.10 for 16, 27.05-27.19 for 48-64, two
+// interleaved rounds on one box (profiles/r03/sweep_aux_cus_r03.log).
 constexpr double kCrossStart = 0.4;
-constexpr int kAuxFreeCUs = 32;
+constexpr int kAuxFreeCUs = 0;
 
 hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
   hipError_t e = hipGetDevice(&c->device);

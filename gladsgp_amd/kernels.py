@@ -350,7 +350,7 @@ def predict_solve(chol: Cholesky, prep: Prepared, s_pred, w,
 
 class FitPredictContext:
     """Caller-owned execution context of :func:`fit_predict` (``gp_ctx_create``): the three
-    library streams (factorisation | CU-masked cross-covariance | prediction) on ``device``.
+    library streams (factorisation | cross-covariance | prediction) on ``device``.
 
     Destroy it with :meth:`close` (or use it as a context manager) while the HIP runtime is up:
     the owner decides the teardown order, the library keeps no global state.
@@ -387,7 +387,7 @@ def fit_predict(X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
                 ctx: FitPredictContext | None = None, check: bool = True):
     """Gram -> Cholesky/L^-1 -> predict for ``batch`` GPs in one gp_fit_predict call.
 
-    With ``ctx`` the cross-covariance runs on the context's CU-masked stream under the
+    With ``ctx`` the cross-covariance runs on the context's own stream under the
     factorisation's latency-bound tail, then the per-chunk TRMM + mean/var; without it every
     step runs in order on the current stream.  ``check`` synchronises and raises if a Gram was
     not positive definite or its factorisation had an internal error (info = -1): the mean /

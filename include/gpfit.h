@@ -200,7 +200,7 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
  *   cross_start  : fraction of the factorisation's n/64 block steps after which the
  *                  cross-covariance starts (< 0: default 0.4; 0 = at once);
  *   aux_free_cus : CUs the cross-covariance stream leaves to the factorisation (CU mask;
- *                  < 0: default 32; 0 = no mask).
+ *                  < 0: default 0 = no mask).
  * gp_ctx_destroy drains the streams and frees them; call it before the HIP runtime is torn
  * down (e.g. before process exit).  A context serves one host thread at a time.
  */
@@ -213,7 +213,7 @@ int gp_ctx_destroy(void* ctx);
  *   mean / var at the m test points (as gp_predict).
  * With ctx == NULL every step runs in order on `stream`.  With a context it forks from
  * `stream` into the context's streams (Gram + factorisation | cross-covariance of every chunk,
- * CU-masked, beside the factorisation | once the factorisation is done z = L^-1 w, then per
+ * beside the factorisation (CU-masked if asked) | once the factorisation is done z = L^-1 w, then per
  * chunk, once that chunk's cross-covariance is done, its TRMM, and one mean/var pass) and joins
  * back: the caller sees one stream-ordered operation.  `ws` holds
  * gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes (the factorisation's scratch included).
