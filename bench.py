@@ -99,52 +99,78 @@ def cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(X, y, beta, Xs, s, delta, sample: int = 20000, reps: int = 3):
-    """numpy fp64 oracle (Gram -> cholesky -> chunked cross-cov + solve_triangular) on the
-    host: full n = 4096 factorisation + prediction of the first ``sample`` test points, timed
-    ``reps`` times (median), extrapolated linearly in the test points to m."""
+def _cpu_c3_run(X, y, beta, Xs, s, delta, sample):
+    """One oracle C3 run on the host: full Gram + Cholesky + alpha, then the first ``sample``
+    test points in 2000-point chunks (cross-covariance, mean, solve_triangular, variance)."""
     from oracle import gp_ref
     import scipy.linalg as sla
+    t0 = time.perf_counter()
+    G = gp_ref.gram_ardse(X, beta, s, delta)
+    L = np.linalg.cholesky(G)
+    alpha = sla.cho_solve((L, True), y)
+    t_fact = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    means, vars_ = [], []
+    for a in range(0, sample, 2000):
+        Ks = gp_ref.cross_ardse(Xs[a:min(sample, a + 2000)], X, beta, s)
+        means.append(Ks @ alpha)
+        V = sla.solve_triangular(L, Ks.T, lower=True, check_finite=False)
+        vars_.append(s - np.einsum("ij,ij->j", V, V))
+    return t_fact, time.perf_counter() - t1, means, vars_
+
+
+def cpu_baseline(X, y, beta, Xs, s, delta, sample: int = 20000, reps: int = 3,
+                 faithful_batches: int = 10):
+    """numpy fp64 oracle (Gram -> cholesky -> chunked cross-cov + solve_triangular) on the
+    host: full n = 4096 factorisation + prediction of the first ``sample`` test points, timed
+    ``reps`` times (median), extrapolated linearly in the test points to m -- with OpenBLAS on
+    the pool's CPU share (``_CPU_THREADS``) and, beside it, on one thread.  Plus the
+    reference-faithful rate: ``faithful_batches`` batches of 4 test points, each re-building
+    and re-factorising the Gram as assess_all_models.py:481-489 does per call."""
+    from oracle import gp_ref
+    import scipy.linalg as sla
+    from threadpoolctl import threadpool_limits
     m = Xs.shape[0]
     sample = min(sample, m)
     runs = []
     for _ in range(reps):
-        t0 = time.perf_counter()
-        G = gp_ref.gram_ardse(X, beta, s, delta)
-        L = np.linalg.cholesky(G)
-        alpha = sla.cho_solve((L, True), y)
-        t_fact = time.perf_counter() - t0
-        t1 = time.perf_counter()
-        means, vars_ = [], []
-        for a in range(0, sample, 2000):
-            Ks = gp_ref.cross_ardse(Xs[a:min(sample, a + 2000)], X, beta, s)
-            means.append(Ks @ alpha)
-            V = sla.solve_triangular(L, Ks.T, lower=True, check_finite=False)
-            vars_.append(s - np.einsum("ij,ij->j", V, V))
-        t_pred = time.perf_counter() - t1
+        t_fact, t_pred, means, vars_ = _cpu_c3_run(X, y, beta, Xs, s, delta, sample)
         runs.append((t_fact + t_pred / sample * m, t_fact, t_pred))
     runs.sort()
     t_full, t_fact, t_pred = runs[len(runs) // 2]
+    s1 = min(2000, m)
+    with threadpool_limits(limits=1):
+        f1, p1, _, _ = _cpu_c3_run(X, y, beta, Xs, s, delta, s1)
+    t_one = f1 + p1 / s1 * m
     # "reference-faithful": re-factorise per batch of 4 points (assess_all_models.py:481-489)
+    nb = max(1, min(faithful_batches, m // 4))
     t2 = time.perf_counter()
-    G4 = gp_ref.gram_ardse(X, beta, s, delta)
-    L4 = np.linalg.cholesky(G4)
-    a4 = sla.cho_solve((L4, True), y)
-    K4 = gp_ref.cross_ardse(Xs[:4], X, beta, s)
-    _ = K4 @ a4, sla.solve_triangular(L4, K4.T, lower=True)
+    for k in range(nb):
+        xb = Xs[4 * k:4 * k + 4]
+        G4 = gp_ref.gram_ardse(X, beta, s, delta)
+        L4 = np.linalg.cholesky(G4)
+        a4 = sla.cho_solve((L4, True), y)
+        K4 = gp_ref.cross_ardse(xb, X, beta, s)
+        _ = K4 @ a4, sla.solve_triangular(L4, K4.T, lower=True)
     t4 = time.perf_counter() - t2
+    aff = len(os.sched_getaffinity(0))
     return {
         "value": m / t_full, "unit": "predictions/s", "cores": _CPU_THREADS, "kind": "port",
         "sample": (f"oracle/gp_ref numpy fp64, OpenBLAS {_CPU_THREADS} threads on "
-                   f"{cpu_model()} (os.cpu_count()={os.cpu_count()}, "
-                   f"affinity={len(os.sched_getaffinity(0))}): full n={X.shape[0]} "
-                   f"Gram+Cholesky + predict of the first {sample} of {m} test points, median of "
-                   f"{reps} runs (fact {t_fact:.2f} s + predict {t_pred:.2f} s), extrapolated "
-                   f"linearly to m={m}"),
-        "reference_faithful_value": 4.0 / t4,
-        "reference_faithful_sample": ("re-factorise per batch of 4 test points as "
-                                      "assess_all_models.py:481-489 does: one batch timed "
-                                      f"({t4:.2f} s)"),
+                   f"{cpu_model()} (os.cpu_count()={os.cpu_count()}, affinity={aff}; the "
+                   f"pool's CPU share per GPU is OMP_NUM_THREADS={_CPU_THREADS}): full "
+                   f"n={X.shape[0]} Gram+Cholesky + predict of the first {sample} of {m} test "
+                   f"points, median of {reps} runs (fact {t_fact:.2f} s + predict "
+                   f"{t_pred:.2f} s), extrapolated linearly to m={m}"),
+        "single_thread_value": m / t_one,
+        "single_thread_sample": (f"the same on 1 OpenBLAS thread (threadpoolctl): fact "
+                                 f"{f1:.2f} s + predict {p1:.2f} s for {s1} points, "
+                                 f"extrapolated to m={m}"),
+        "reference_faithful_value": 4.0 * nb / t4,
+        "reference_faithful_sample": (f"re-factorise per batch of 4 test points as "
+                                      f"assess_all_models.py:481-489 does: {nb} batches "
+                                      f"({4 * nb} test points) timed, {t4:.2f} s, "
+                                      f"{_CPU_THREADS} threads"),
     }, np.concatenate(means), np.concatenate(vars_)
 
 
@@ -271,6 +297,13 @@ def main():
                     help="testing only: every rank on cuda:0 over gloo (host-staged collectives)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: headline = the redundant-factorisation strong split only")
+    ap.add_argument("--force-nccl", action="store_true",
+                    help="join an RCCL process group even at N = 1, so every collective "
+                         "branch of the N > 1 path (broadcast, gather, barrier, the pipelined "
+                         "schedule) runs through a one-rank RCCL communicator")
+    ap.add_argument("--cpu-faithful-batches", type=int, default=10,
+                    help="reference-faithful CPU leg: batches of 4 test points timed "
+                         "(assess_all_models.py:481-489 re-factorises per batch)")
     ap.add_argument("--workload", choices=("c3", "c4", "fit", "latency"), default="c3")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rendezvous / JSON path only, no GPU work (gloo on the host)")
@@ -304,7 +337,8 @@ def main():
         return main_latency(args)
 
     ctx = (gdist.init_from_env("cuda", backend="gloo", device_index=0) if args.share_gpu
-           else gdist.init_from_env("cuda"))
+           else gdist.init_from_env("cuda", force_group=args.force_nccl))
+    multi = ctx.world > 1 or args.force_nccl      # the N > 1 schedule (collectives included)
     if ctx.world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but {ctx.world} ranks joined "
                          "(WORLD_SIZE); refusing to report a mislabelled number")
@@ -384,7 +418,7 @@ def main():
     if fctx is not None:
         fctx.close()
     pipe = None
-    if ctx.world > 1 and not args.no_pipeline:
+    if multi and not args.no_pipeline:
         pipe = c3_pipelined(args, ctx, X, y, beta, Xs, s, delta, timed)
     if ctx.rank != 0:
         return
@@ -446,10 +480,15 @@ def main():
                    "n_train": n, "m_test": m, "d": d, "m_test_rank0": ml,
                    "parallelism": (f"strong: m/{ctx.world} test-point blocks per rank, "
                                    "redundant factorisation, (mean, var) gathered to rank 0 "
-                                   "every step" if ctx.world > 1 else "1 GPU"),
+                                   "every step" if multi else "1 GPU"),
                    "pipeline": ("serial (one stream)" if args.serial else
-                                "gp_fit_predict on a gp_ctx (cross-covariance on a CU-masked "
-                                "stream beside the factorisation)")},
+                                "gp_fit_predict on a gp_ctx (cross-covariance on the "
+                                "context's aux stream, no CU mask, beside the "
+                                "factorisation)"),
+                   "collectives": (f"{ctx.backend} process group of {ctx.world}"
+                                   + (" (--force-nccl: one-rank RCCL rehearsal of the N > 1 "
+                                      "path)" if args.force_nccl and ctx.world == 1 else "")
+                                   if ctx.distributed else "none (single process)")},
         "roofline": roof, "roofline_aux": aux, "weak": weak, "cpu_baseline": None,
     }
     if res is None or tuple(res.shape) != (2, m):
@@ -475,7 +514,8 @@ def main():
         line["pipeline"] = {"t_fact_ms": pipe["t_fact_ms"], "t_point_us": pipe["t_point_us"],
                             "check_last_step_vs_direct": pipe["check"]}
     if ctx.world == 1 and not args.no_cpu:
-        cb, mu_ref, var_ref = cpu_baseline(X, y, beta, Xs, s, delta, args.cpu_sample)
+        cb, mu_ref, var_ref = cpu_baseline(X, y, beta, Xs, s, delta, args.cpu_sample,
+                                           faithful_batches=args.cpu_faithful_batches)
         k = mu_ref.shape[0]
         mu_g = res[0, :k].cpu().numpy()
         var_g = res[1, :k].cpu().numpy()
@@ -491,7 +531,7 @@ C4_DEFAULT_CHUNK = 8192   # the library's default test-point chunk for a batch (
 
 def main_c4(args):
     from gladsgp_amd.emulator import assemble_units
-    ctx = gdist.init_from_env("cuda")
+    ctx = gdist.init_from_env("cuda", force_group=args.force_nccl)
     dev = ctx.device
     n = args.n if args.n != 4096 else 1024
     m, d, P = args.m, args.d, args.pcs
@@ -572,6 +612,8 @@ def main_c4(args):
                                "predict, gather to rank 0",
                    "pcs": P, "n_train": n, "m_test": m, "d": d,
                    "parallelism": f"PC shards x{ctx.world} (RCCL broadcast + gather)",
+                   "collectives": (f"{ctx.backend} process group of {ctx.world}"
+                                   if ctx.distributed else "none (single process)"),
                    "path": args.c4_path},
         "roofline": {"kernel": "trmm_pair_kernel (rank 0's PCs)", "bound": "mfma",
                      "achieved": round(tr_tfs, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
@@ -794,4 +836,9 @@ def main_fit(args):
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    finally:
+        import torch.distributed as _tdist
+        if _tdist.is_available() and _tdist.is_initialized():
+            _tdist.destroy_process_group()

@@ -103,6 +103,7 @@ SIGNATURES = {
     "gp_profile_reset": (c_int, []),
     "gp_profile_read": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
     "gp_set_poll_budget": (c_ll, [c_ll]),
+    "gp_set_potrf_path": (c_int, [c_int]),
 }
 
 PROF_GRAM, PROF_POTRF, PROF_TRMM, PROF_CROSS = 0, 1, 2, 3

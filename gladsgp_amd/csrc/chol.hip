@@ -1860,10 +1860,12 @@ static bool pp_shape_ok(int n, int batch) {
   return N <= kPPMaxN && pp_task_count(N, true) * (long long)batch < (1ll << 30);
 }
 
+// gp_set_potrf_path (test / A-B hook): 1 forces the blocked sweep for later factorisations
+static int g_potrf_path = 0;
+
 static bool pp_eligible(int n, int batch, int resident) {
   // the chains hold `batch` workgroups for the whole launch: at least as many workers again
-  return pp_shape_ok(n, batch) && 2 * batch <= resident &&
-         std::getenv("GPFIT_POTRF_SWEEP") == nullptr;
+  return g_potrf_path == 0 && pp_shape_ok(n, batch) && 2 * batch <= resident;
 }
 
 // The persistent dataflow factorisation (pp_kernel) on `stream` in the caller's scratch `scr`
@@ -2104,6 +2106,14 @@ extern "C" int gp_trtri(const double* L, int n, int ldl, long long strideL, doub
 extern "C" long long gp_set_poll_budget(long long polls) {
   const long long prev = g_poll_budget;
   g_poll_budget = polls == 0 ? kPollBudget : polls;
+  return prev;
+}
+
+// Factorisation path for later enqueues (process-wide test / A-B hook): 0 = automatic (the
+// persistent kernel where eligible), 1 = always the blocked sweep.  Returns the previous value.
+extern "C" int gp_set_potrf_path(int path) {
+  const int prev = g_potrf_path;
+  g_potrf_path = path == 1 ? 1 : 0;
   return prev;
 }
 

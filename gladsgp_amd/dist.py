@@ -37,12 +37,15 @@ class Context:
 
 
 def init_from_env(device_type: str | None = None, backend: str | None = None,
-                  device_index: int | None = None) -> Context:
+                  device_index: int | None = None, force_group: bool = False) -> Context:
     """Join the process group described by RANK/WORLD_SIZE/MASTER_* (torchrun), if any.
 
     Defaults: one GPU per rank (cuda:LOCAL_RANK) over RCCL.  ``backend="gloo"`` with
     ``device_index`` lets several ranks share one GPU (the multi-rank GPU tests on a 1-GPU box;
-    collectives then stage through the host)."""
+    collectives then stage through the host).  ``force_group``: join a process group even at
+    world size 1 (RCCL accepts a one-rank communicator), so every collective branch of the
+    sharded paths runs exactly as it does on N GPUs -- the one-GPU rehearsal of the RCCL code
+    path (``bench.py --force-nccl``, ``tests/test_gpu_rccl.py``)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -54,15 +57,26 @@ def init_from_env(device_type: str | None = None, backend: str | None = None,
         device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
-    if world > 1:
+    if world > 1 or force_group:
         backend = backend or ("nccl" if device_type == "cuda" else "gloo")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                os.environ["MASTER_PORT"] = str(_free_port())
             kw = {"device_id": device} if backend == "nccl" else {}
             dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     else:
         backend = None
     return Context(rank, world, local_rank, device, backend)
+
+
+def _free_port() -> int:
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
 
 
 def barrier(ctx: Context) -> None:

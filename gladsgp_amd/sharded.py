@@ -113,12 +113,15 @@ def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta,
     if mode not in ("redundant", "broadcast"):
         raise ValueError(f"mode must be 'redundant' or 'broadcast', got {mode!r}")
     dev = X.device
-    world = ctx.world if ctx is not None and ctx.distributed else 1
-    rank = ctx.rank if world > 1 else 0
+    # collectives run whenever there is a process group, also at world size 1 (an RCCL
+    # communicator of one rank exercises the same code path as the N-GPU runs)
+    dist_on = ctx is not None and ctx.distributed
+    world = ctx.world if dist_on else 1
+    rank = ctx.rank if dist_on else 0
     m = Xs.shape[0]
     n = X.shape[0]
     if counts is None:
-        if mode == "broadcast" and world > 1:
+        if mode == "broadcast" and dist_on:
             t_fact, t_point = calibrate(ctx, X, Xs, beta, s, delta, s_pred, w)
             counts = split_counts(m, world, t_fact / t_point)
         else:
@@ -129,7 +132,7 @@ def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta,
     hi = lo + counts[rank]
     Xl = Xs[lo:hi].contiguous()
     buf = torch.empty((2, max(hi - lo, 1)), dtype=F64, device=dev)
-    if mode == "redundant" or world == 1:
+    if mode == "redundant" or not dist_on:
         if hi > lo:
             kernels.fit_predict(X, Xl, beta, s, delta, s_pred, w, m_chunk=m_chunk,
                                 workspace=workspace, out=(buf[0:1, : hi - lo],
@@ -159,7 +162,7 @@ def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta,
     mine = buf[:, : hi - lo]
     if not gather:
         return mine[0], mine[1], (lo, hi)
-    if world == 1:
+    if not dist_on:
         return mine[0], mine[1]
     res = gdist.gather_cols(ctx, mine.contiguous(), counts)
     if res is None:
@@ -221,11 +224,12 @@ class PipelinedPredictor:
         self.m = Xs.shape[0]
         self.w = w.reshape(1, self.n).contiguous()
         self.m_chunk = m_chunk
-        world = ctx.world if ctx.distributed else 1
-        self.world, self.rank = world, (ctx.rank if ctx.distributed else 0)
+        self.dist = ctx is not None and ctx.distributed   # collectives (also at world 1)
+        world = ctx.world if self.dist else 1
+        self.world, self.rank = world, (ctx.rank if self.dist else 0)
         self.t_fact = self.t_point = None
         if counts is None:
-            if world > 1:
+            if self.dist and (world > 1 or calib_gp is not None):
                 if calib_gp is None:
                     raise ValueError("PipelinedPredictor: give counts or a calib_gp")
                 b, s_, d_, sp = calib_gp[:4]
@@ -275,7 +279,7 @@ class PipelinedPredictor:
     def _bcast(self, slot: int):
         if self.rank == 0:
             self.packer.pack(self.linv[slot], self.info, self.packed[slot])
-        if self.world == 1:
+        if not self.dist:
             return None
         return _wire_bcast(self.ctx, self.packed[slot], async_op=True)
 
@@ -300,7 +304,7 @@ class PipelinedPredictor:
             nxt_req = self._bcast(nxt)
         if self.pending is not None:
             self.pending.wait()
-        if self.rank != 0 and self.world > 1:
+        if self.rank != 0:
             self.packer.unpack(self.packed[cur], self.linv[cur])
         got = self.packer.info(self.packed[cur])
         self.status.copy_(torch.where(self.status != 0, self.status, got))
@@ -311,7 +315,7 @@ class PipelinedPredictor:
                             workspace=self.ws, out=(self.out[0:1, : self.ml],
                                                     self.out[1:2, : self.ml]))
         res = gdist.gather_cols(self.ctx, self.out[:, : self.ml], self.counts) \
-            if self.world > 1 else self.out[:, : self.ml]
+            if self.dist else self.out[:, : self.ml]
         self.pending = nxt_req
         self.k = k + 1
         return res

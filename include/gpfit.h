@@ -401,6 +401,12 @@ int gp_profile_read(int id, int* count, double* total_ms, double* max_ms);
  * captured with.  Returns the previous setting. */
 long long gp_set_poll_budget(long long polls);
 
+/* Test / A-B hook, process-wide: the factorisation path of gp_potrf_inv / gp_potrf /
+ * gp_fit_predict / gp_loglik enqueued afterwards.  0 = automatic (the persistent dataflow
+ * kernel where eligible, else the blocked sweep), 1 = always the blocked right-looking sweep.
+ * Returns the previous setting. */
+int gp_set_potrf_path(int path);
+
 #ifdef __cplusplus
 }
 #endif

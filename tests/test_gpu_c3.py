@@ -88,3 +88,25 @@ def test_c3_permutation_equivariance(c3):
     np.testing.assert_allclose(mean, c3["mean"][perm], rtol=0,
                                atol=1e-13 * np.abs(c3["mean"]).max())
     np.testing.assert_allclose(var, c3["var"][perm], rtol=0, atol=1e-13 * c3["s"])
+
+
+def test_c3_bench_path_context_defaults(c3):
+    """The bench's own headline path (time_predictions.py:73-79 at C3 size): gp_fit_predict on a
+    gp_ctx with the library defaults (cross-covariance on the context's unmasked aux stream
+    beside the factorisation, per-chunk events), twice on one context and through the bench's
+    caller-owned workspace and output views -- bit-identical to the serial one-stream result the
+    oracle check above pins."""
+    from gladsgp_amd import kernels
+    t = c3["t"]
+    ws = kernels.PredictWorkspace()
+    out = torch.empty((2, M), dtype=torch.float64, device=t["X"].device)
+    with kernels.FitPredictContext(t["X"].device) as fctx:
+        for _ in range(2):
+            out.fill_(float("nan"))
+            _, _, ch = kernels.fit_predict(t["X"], t["Xs"], t["beta"], t["s"], t["delta"], t["s"],
+                                           t["y"], workspace=ws, out=(out[0:1], out[1:2]),
+                                           ctx=fctx, check=False)
+            torch.cuda.synchronize()
+            ch.check()
+            res = out.cpu().numpy()
+            assert np.array_equal(res[0], c3["mean"]) and np.array_equal(res[1], c3["var"])

@@ -10,7 +10,6 @@ both factorisation paths (persistent groups and the blocked sweep) against the o
 
 Tolerances: |dmean| <= 1e-9 max(1, |mean|), |dvar| <= 1e-9 (s ~ 0.3-2).
 """
-import os
 
 import numpy as np
 import pytest
@@ -86,15 +85,24 @@ def test_reference_prediction_shapes(dev, tmp_path, n, S, group):
     assert np.all(pred.var > 0)
 
 
+@pytest.fixture
+def force_sweep():
+    """gp_set_potrf_path(1) (the ABI's test hook) for the test, restored afterwards."""
+    from gladsgp_amd import _capi
+    prev = _capi.lib().gp_set_potrf_path(1)
+    yield
+    _capi.lib().gp_set_potrf_path(prev)
+
+
 @pytest.mark.parametrize("sweep", [False, True])
-def test_cholesky_inverse_batch_256_n512(dev, sweep, monkeypatch):
+def test_cholesky_inverse_batch_256_n512(dev, sweep, request):
     """One cholesky_inverse of 256 n = 512 Grams (beyond the persistent kernel's batch limit:
-    the blocked sweep), and the same with GPFIT_POTRF_SWEEP forcing the sweep at a batch the
+    the blocked sweep), and the same with gp_set_potrf_path(1) forcing the sweep at a batch the
     persistent kernel would take (128)."""
     from gladsgp_amd import kernels
     B = 256 if not sweep else 128
     if sweep:
-        monkeypatch.setenv("GPFIT_POTRF_SWEEP", "1")
+        request.getfixturevalue("force_sweep")
     n = 512
     rng = np.random.default_rng(31)
     X = rng.random((n, 8))
@@ -116,7 +124,7 @@ def test_cholesky_inverse_batch_256_n512(dev, sweep, monkeypatch):
                                    rtol=0, atol=1e-9 * n)
 
 
-def test_sweep_multi_tile_matches_persistent(dev, monkeypatch):
+def test_sweep_multi_tile_matches_persistent(dev):
     """The sweep and the persistent kernel agree at a multi-tile shape with ragged tiles."""
     from gladsgp_amd import kernels
     rng = np.random.default_rng(17)
@@ -124,12 +132,16 @@ def test_sweep_multi_tile_matches_persistent(dev, monkeypatch):
     X = rng.random((n, 8))
     betas = rng.uniform(0.5, 5, (B, 8))
     G = kernels.gram(_t(X, dev), _t(betas, dev), 1.0, 1e-4)
+    from gladsgp_amd import _capi
     a = kernels.cholesky_inverse(G.clone())
-    monkeypatch.setenv("GPFIT_POTRF_SWEEP", "1")
-    b = kernels.cholesky_inverse(G.clone())
+    prev = _capi.lib().gp_set_potrf_path(1)
+    try:
+        b = kernels.cholesky_inverse(G.clone())
+        torch.cuda.synchronize()
+    finally:
+        assert _capi.lib().gp_set_potrf_path(prev) == 1
     for c in (a, b):
         assert c.info.cpu().tolist() == [0] * B
     La, Lb = a.L.cpu().numpy(), b.L.cpu().numpy()
     for k in range(B):
         assert np.max(np.abs(La[k] - Lb[k])) <= 1e-11 * np.max(np.abs(La[k]))
-    assert os.environ.get("GPFIT_POTRF_SWEEP") == "1"

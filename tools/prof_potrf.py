@@ -1,6 +1,8 @@
 """Profile target: gram + potrf_inv at n (default 4096), `batch` problems, a few times.
 
     python tools/prof_potrf.py [n] [reps] [batch]
+
+GPFIT_POTRF_SWEEP=1 in the environment: this tool sets gp_set_potrf_path(1) (the blocked sweep).
 """
 import os
 import sys
@@ -10,7 +12,10 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from gladsgp_amd import kernels  # noqa: E402
+from gladsgp_amd import _capi, kernels  # noqa: E402
+
+if os.environ.get("GPFIT_POTRF_SWEEP") == "1":
+    _capi.lib().gp_set_potrf_path(1)
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
