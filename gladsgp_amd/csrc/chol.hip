@@ -196,6 +196,9 @@ using LdsSmem = __attribute__((address_space(3))) Smem;
 // fixed address in all of them and diag_factor_inv (a separate function) addresses it with
 // immediate offsets instead of a runtime base register.
 __shared__ Smem g_sm;
+// chain: L_j+1,j as [p][r] (opA layout) between steps, the two-wave leaf's multipliers during
+// the diagonal factor; workers: the XT pair's third tile
+__shared__ double g_keep[NB * LP];
 using lds_double = __attribute__((address_space(3))) double;
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 using lds_dvec2 = __attribute__((address_space(3))) const dvec2;
@@ -946,7 +949,6 @@ int* g_trace_dbg = nullptr;         // gp_pp_trace_set (trace build only)
 long long* g_trace_buf = nullptr;
 #endif
 
-__shared__ double g_keep[NB * LP];    // chain: L_j+1,j as [p][r] (opA layout) between steps
 __shared__ int g_msg[4];              // dequeued task / wait results broadcast to the workgroup
 
 struct PPArgs {
