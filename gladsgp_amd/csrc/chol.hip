@@ -940,6 +940,16 @@ constexpr int kTChain = 0, kTL = 1, kTDP = 2, kTSP = 3, kTX = 4;
 // more (n = 4096 2.07 vs 1.84 ms, profiles/r03/ab_libs_pp7.log): removed.
 constexpr int kPPXTailRows = 8;
 constexpr int kTX2 = 6;     // XT pair: X_ic and X_i,c+1 (one opA stream, two opB streams)
+// Zero tasks (inv only): the parts of the padded L^-1 buffer the factorisation never writes --
+// the upper tiles (r, c), r < c < NT = npad / 64, kPPZRun of them per task (one tile column), and
+// when npad / 64 = N + 1 the pure-padding tile row N (kTZP, 8 tile columns per task) -- so the
+// buffer meets gp_potrf_inv's contract (zero above the diagonal and in the padding) without the
+// caller-stream memset of the whole npad^2 buffer (134 MB at n = 4096: 18 us ahead of every
+// factorisation).  They sit in the first keys, which hold no other task: the workers take them
+// while the chain factors its first diagonal block, which every other early task waits on.
+constexpr int kTZ = 5, kTZP = 7;
+constexpr int kPPZRun = 8;       // tiles per zero task (256 KB)
+constexpr int kPPZKeys = 4;      // keys 0..3 (the first worker tasks are at key 4)
 constexpr long long kPollBudget = 1ll << 22;   // default s_sleep polls before a wait gives up
 // gp_set_poll_budget (test / diagnostics hook): polls per wait for later launches; < 0 starts
 // every problem aborted (the deterministic abort path of the tests)
@@ -1088,7 +1098,8 @@ GP_DEV void pp_store_cm(double* dst, int ld, const double* Cs, int rv, int cv, b
 // Store the nb x nb tile held in LDS as T[row][col] (pitch LP) to dst (col-major, ld) with sc1
 // stores: 16-B pairs of rows for a full aligned tile, else 8-B elements; `lower`: only
 // row >= col (LAPACK: the strict upper triangle of A is never written).
-GP_DEV void pp_store_rm(double* dst, int ld, const double* T, int nb, bool lower) {
+GP_DEV void pp_store_rm(double* dst, int ld, const double* T, int nb, bool lower,
+                        bool zpad = false) {
   const int tid = threadIdx.x;
   const bool full = nb == NB && (ld & 1) == 0 && (((size_t)dst & 15) == 0);
   if (full) {
@@ -1113,9 +1124,10 @@ GP_DEV void pp_store_rm(double* dst, int ld, const double* T, int nb, bool lower
     for (int q = 0; q < 16; ++q) {
       int row, col;
       slot_rc(q, row, col);
-      if (row < nb && col < nb && (!lower || row >= col))
-        __hip_atomic_store(dst + row + (long long)col * ld, T[row * LP + col], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      const bool in = row < nb && col < nb;
+      if ((in && (!lower || row >= col)) || (zpad && !in))
+        __hip_atomic_store(dst + row + (long long)col * ld, in ? T[row * LP + col] : 0.0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1538,7 +1550,7 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
     double* D = pp_dptr(P, b, j, ldd);
     if (j + 1 >= N) {
       // last step: D_j -> X_jj (or the D scratch), L_jj -> A (lower, LAPACK layout)
-      pp_store_rm(D, ldd, sm.Bs, nb, false);
+      pp_store_rm(D, ldd, sm.Bs, nb, false, true);
       pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);
       pp_publish(F + j * N + j);
       PP_TRACE(P, tb0 + 4, pp_now());
@@ -1550,14 +1562,19 @@ GP_DEV void pp_chain(const PPArgs& P, int b) {
     // the next P_j+1,j+1 go out with the stores when their partial sums are already published.
     PP_MARK(P, 13, j);
     const int nb1 = min(NB, P.n - (j + 1) * NB);
-    pp_store_rm(D, ldd, sm.Bs, nb, false);
-    pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);   // L_jj: read by nobody in this launch
+    // (zero padding past nb: X's rows >= n come out 0 in the XT tasks)
+    pp_store_rm(D, ldd, sm.Bs, nb, false, true);
     OpTile tp;
     const bool spref = j < 1 || pp_test1(F + 2 * N * N + N + j);
     if (spref) pp_load(tp, atile(j + 1, j), P.lda, nb1, NB);
     pref = j + 1 < 2 || pp_test1(F + 2 * N * N + j + 1);
     if (pref) pp_load(tpj, atile(j + 1, j + 1), P.lda, nb1, nb1);
     pp_publish(F + j * N + j);                          // drains stores and loads alike
+    // L_jj (read by nobody in this launch) after D_j's flag: its stores drain under the GEMM
+    // instead of in front of the flag (n = 4096 1.812 vs 1.824 ms, n = 1024 x 32 0.994 vs
+    // 0.998, bit-identical; profiles/r04/ab_zt_ljj.log)
+    pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);
+    __syncthreads();                                    // every wave has read As
     PP_TRACE(P, tb0 + 4, pp_now());
     if (!spref) {
       if (!pp_wait1(F + 2 * N * N + N + j, abort, P.budget)) return;
@@ -1599,6 +1616,35 @@ GP_DEV void pp_exit(const PPArgs& P) {
   }
 }
 
+// Zero task: plain 16-B stores (read only by later launches: the kernel boundary orders them).
+GP_DEV void pp_zero(const PPArgs& P, const PPTask& T) {
+  double* Xb = P.X + T.b * P.sX;
+  const int NT = (P.N + 1) & ~1;
+  int r0, r1, c0, c1;                          // rows [64 r0, 64 r1) x columns [64 c0, 64 c1)
+  if (T.kind == kTZ) {
+    c0 = T.i; c1 = T.i + 1;
+    r0 = T.j; r1 = min(T.j + kPPZRun, T.i);
+  } else {
+    c0 = T.i; c1 = min(T.i + 8, NT);
+    r0 = P.N; r1 = NT;
+  }
+  const int rows = NB * (r1 - r0), cols = NB * (c1 - c0);
+  double* base = Xb + (long long)NB * r0 + (long long)NB * c0 * P.ldx;
+  if ((P.ldx & 1) == 0 && ((size_t)Xb & 15) == 0) {
+    const int h = rows / 2;                    // double2 per column
+    const double2 z2 = make_double2(0.0, 0.0);
+    for (int g = threadIdx.x; g < h * cols; g += 256) {
+      const int col = g / h, e = g - col * h;
+      *reinterpret_cast<double2*>(base + (long long)col * P.ldx + 2 * e) = z2;
+    }
+  } else {
+    for (int g = threadIdx.x; g < rows * cols; g += 256) {
+      const int col = g / rows, e = g - col * rows;
+      base[(long long)col * P.ldx + e] = 0.0;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
   for (;;) {
     if (threadIdx.x == 0) g_msg[0] = atomicAdd(P.head, 1);
@@ -1626,6 +1672,16 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
       continue;
     }
     T.idx = t;
+    if (T.kind == kTZ || T.kind == kTZP) {
+      PP_TRACE(P, (long long)t * 6 + 1, pp_now());
+      pp_zero(P, T);
+      PP_TRACE(P, (long long)t * 6 + 0, blockIdx.x);
+      PP_TRACE(P, (long long)t * 6 + 2, pp_now());
+      PP_TRACE(P, (long long)t * 6 + 3, pp_now());
+      PP_TRACE(P, (long long)t * 6 + 4, T.kind | (T.b << 4));
+      PP_TRACE(P, (long long)t * 6 + 5, T.i | (T.j << 16));
+      continue;
+    }
     T.nterms = T.kind == kTL ? T.j : T.kind == kTDP ? T.j - 1 : T.kind == kTSP ? T.j : T.i - T.j;
     pp_worker(P, T);
   }
@@ -1666,6 +1722,13 @@ constexpr int kPPXDelay = 8;   // XT tasks: 8 chain steps after the late LT task
 // section comment).  Shared by the schedule kernel (count + emit) and the host's task count.
 template <typename F>
 GP_HD inline void pp_for_key(int t, int N, bool inv, int lead, int xd, F&& f) {
+  if (inv && t < kPPZKeys) {
+    const int NT = (N + 1) & ~1;                               // npad / 64
+    for (int c = 1 + t; c < NT; c += kPPZKeys)
+      for (int r0 = 0; r0 < c; r0 += kPPZRun) f(kTZ, c, r0);
+    if (t == 0 && NT > N)
+      for (int c0 = 0; c0 < NT; c0 += 8) f(kTZP, c0, 0);
+  }
   // late tasks of this position first (K = t - 4W): a late task can be an input of an early
   // task of the same position, never the other way round
   const int K = t - 4 * lead;
@@ -1986,7 +2049,8 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
     if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
     if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
   }
-  GP_CK(zero_linv(Linv, npad, ldinv, strideInv, batch, stream));
+  // the persistent kernel zeroes what it does not write itself (its zero tasks)
+  if (!pp) GP_CK(zero_linv(Linv, npad, ldinv, strideInv, batch, stream));
   gpfit_prof_begin(GP_PROF_POTRF, stream);
   int rc;
   if (pp) {

@@ -105,6 +105,42 @@ def test_cholesky_inverse(dev, n):
     assert np.all(full[n:, :] == 0) and np.all(full[:, n:] == 0)
 
 
+@pytest.mark.parametrize("n,B", [(5, 1), (65, 2), (129, 1), (700, 2), (1000, 1)])
+def test_cholesky_inverse_poisoned_buffer(dev, n, B):
+    """The factorisation writes every entry of the padded L^-1 buffer itself -- the persistent
+    kernel's zero tasks (upper tiles, pure-padding tile row / column) and its zero-padded
+    diagonal blocks replace the caller-stream memset (round 4) -- so a buffer pre-filled with
+    NaN comes back exactly zero above the diagonal and in the padding, and the same L^-1 as a
+    zero-filled one."""
+    from gladsgp_amd import _capi, kernels
+    rng = np.random.default_rng(100 + n)
+    X = rng.random((n, 8))
+    G = np.stack([gp_ref.gram_ardse(X, rng.uniform(0.5, 5, 8), 1.0, 1e-4) for _ in range(B)])
+    npad = kernels.padded_n(n)
+    ws_b = int(_capi.lib().gp_potrf_inv_ws_bytes(n, B))
+    ws = torch.empty(max(ws_b, 256), dtype=torch.uint8, device=dev)
+    outs = []
+    for fill in (float("nan"), 0.0):
+        A = _t(G, dev).contiguous()
+        Linv = torch.full((B, npad, npad), fill, dtype=torch.float64, device=dev)
+        info = torch.empty(B, dtype=torch.int32, device=dev)
+        logdet = torch.empty(B, dtype=torch.float64, device=dev)
+        _capi.call("gp_potrf_inv_ws", A.data_ptr(), n, n, n * n, Linv.data_ptr(), npad,
+                   npad * npad, B, info.data_ptr(), logdet.data_ptr(), ws.data_ptr(),
+                   ws.numel(), torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+        assert info.cpu().tolist() == [0] * B
+        outs.append(Linv.transpose(1, 2).cpu().numpy())          # [b][row][col]
+    full = outs[0]
+    assert np.all(np.isfinite(full))
+    for b in range(B):
+        assert np.all(np.triu(full[b], 1) == 0)
+        assert np.all(full[b][n:, :] == 0) and np.all(full[b][:, n:] == 0)
+        Lref = np.linalg.cholesky(G[b])
+        assert np.max(np.abs(full[b][:n, :n] @ Lref - np.eye(n))) <= 1e-9
+    assert np.array_equal(full, outs[1])
+
+
 def test_cholesky_upper_triangle_untouched(dev):
     from gladsgp_amd import kernels
     rng = np.random.default_rng(2)

@@ -45,7 +45,7 @@ t = trace.cpu().numpy()
 tk = t[: nt * SL].reshape(nt, SL).astype(np.float64)
 kinds_raw = t[: nt * SL].reshape(nt, SL)[:, 4] & 15
 ij = t[: nt * SL].reshape(nt, SL)[:, 5]
-KN = {1: "L", 2: "DP", 3: "SP", 4: "X", 6: "X2"}
+KN = {1: "L", 2: "DP", 3: "SP", 4: "X", 5: "Z", 6: "X2", 7: "ZP"}
 tasks = [("C", 0, 0) if kinds_raw[k] == 0 else (KN[int(kinds_raw[k])], int(ij[k] & 0xffff),
                                                 int(ij[k] >> 16)) for k in range(nt)]
 cs = t[nt * SL:].reshape(N, 8).astype(np.float64)
