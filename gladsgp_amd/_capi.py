@@ -84,6 +84,9 @@ SIGNATURES = {
     "gp_dgemm": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.c_double, c_void_p, c_int,
                          c_void_p, c_int, ctypes.c_double, c_void_p, c_int, c_void_p, c_ll,
                          c_void_p]),
+    "gp_gemm_ex": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.c_double, c_void_p, c_int,
+                           c_int, c_void_p, c_int, c_int, ctypes.c_double, c_void_p, c_int,
+                           c_void_p, c_ll, c_void_p]),
     "gp_sim_stats": (c_int, [c_void_p, c_int, c_int, c_ll, ctypes.c_double, c_void_p, c_void_p,
                              c_void_p]),
     "gp_standardize": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_ll,

@@ -23,6 +23,11 @@ class CM:
     cols: int
     ld: int
 
+    @property
+    def f32(self) -> bool:
+        """Stored as float32 (read by gp_gemm_ex and widened to fp64 on load)."""
+        return self.t.dtype == torch.float32
+
     @staticmethod
     def empty(rows: int, cols: int, device) -> "CM":
         t = torch.empty((max(cols, 1), max(rows, 1)), dtype=F64, device=device)
@@ -62,7 +67,9 @@ def _ws(nbytes: int, device) -> torch.Tensor | None:
 
 def gemm(transa: bool, transb: bool, A: CM, B: CM, alpha: float = 1.0, beta: float = 0.0,
          C: CM | None = None) -> CM:
-    """C = alpha op(A) op(B) + beta C on MFMA (split-K for long inner dimensions)."""
+    """C = alpha op(A) op(B) + beta C on MFMA (split-K for long inner dimensions).  A or B may
+    be float32 (gp_gemm_ex widens them on load: the same fp64 result as on an fp64 copy); C is
+    fp64."""
     m = A.cols if transa else A.rows
     k = A.rows if transa else A.cols
     kb = B.cols if transb else B.rows
@@ -76,8 +83,13 @@ def gemm(transa: bool, transb: bool, A: CM, B: CM, alpha: float = 1.0, beta: flo
     lib = _capi.lib()
     nbytes = lib.gp_dgemm_ws_bytes(m, n, k)
     ws = _ws(nbytes, dev)
-    _capi.call("gp_dgemm", int(transa), int(transb), m, n, k, float(alpha), A.ptr(), A.ld,
-               B.ptr(), B.ld, float(beta), C.ptr(), C.ld,
+    for nm, M in (("A", A), ("B", B)):
+        if M.t.dtype not in (torch.float32, F64):
+            raise TypeError(f"gemm: {nm} must be float32 or float64, got {M.t.dtype}")
+    if C.t.dtype != F64:
+        raise TypeError("gemm: C must be float64")
+    _capi.call("gp_gemm_ex", int(transa), int(transb), m, n, k, float(alpha), A.ptr(),
+               int(A.f32), A.ld, B.ptr(), int(B.f32), B.ld, float(beta), C.ptr(), C.ld,
                ws.data_ptr() if ws is not None else None, nbytes if ws is not None else 0,
                _stream(dev))
     return C

@@ -16,30 +16,45 @@ namespace {
 constexpr int TB = 64;
 constexpr int TP = TB + 1;
 
-// S[k][x] = op(M)(x, k) for a 64x64 block at (x0, k0); NAT: M[x + k*ld], TRN: M[k + x*ld].
-template <bool TRN>
-GP_DEV void stage_g(double* S, const double* __restrict__ M, int ld, int x0, int xmax, int k0,
-                    int kmax) {
-#pragma unroll 4
-  for (int q = 0; q < (TB * TB) / 256; ++q) {
+// Operand staging of one 64 x 64 K-step: S[k][x] = op(M)(x, k) for the block at (x0, k0);
+// NAT: M[x + k*ld], TRN: M[k + x*ld].  Thread slot q reads element (fast, slow) = (g & 63,
+// g >> 6), g = tid + 256 q, so a wave reads 64 consecutive elements of memory; the element type
+// E (double, or float widened exactly on load -- the fit's float32 ensembles are read as
+// stored, without an fp64 copy) only changes the load.  Split in two phases so the next
+// K-step's loads are in flight while the current one's MFMAs run.
+template <bool TRN, typename E>
+GP_DEV void stage_load(double (&r)[16], const E* __restrict__ M, int ld, int x0, int xmax,
+                       int k0, int kmax) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
     const int g = threadIdx.x + 256 * q;
     const int fast = g & (TB - 1), slow = g >> 6;
     int x, k;
     if (!TRN) { x = fast; k = slow; } else { k = fast; x = slow; }
     const int gx = x0 + x, gk = k0 + k;
-    double v = 0.0;
-    if (gx < xmax && gk < kmax)
-      v = TRN ? M[gk + (long long)gx * ld] : M[gx + (long long)gk * ld];
-    S[k * TP + x] = v;
+    r[q] = (gx < xmax && gk < kmax)
+               ? static_cast<double>(TRN ? M[gk + (long long)gx * ld] : M[gx + (long long)gk * ld])
+               : 0.0;
+  }
+}
+
+template <bool TRN>
+GP_DEV void stage_store(double* S, const double (&r)[16]) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int g = threadIdx.x + 256 * q;
+    const int fast = g & (TB - 1), slow = g >> 6;
+    const int x = TRN ? slow : fast, k = TRN ? fast : slow;
+    S[k * TP + x] = r[q];
   }
 }
 
 // opA(i,k): transa=0 -> A[i + k*lda] (NAT staging), 1 -> A[k + i*lda] (TRN staging)
 // opB(k,j): transb=0 -> B[k + j*ldb] (TRN staging), 1 -> B[j + k*ldb] (NAT staging)
-template <int TA, int TBT>
+template <int TA, int TBT, typename EA, typename EB>
 __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, int kchunk,
-                                                   const double* __restrict__ A, int lda,
-                                                   const double* __restrict__ B, int ldb,
+                                                   const EA* __restrict__ A, int lda,
+                                                   const EB* __restrict__ B, int ldb,
                                                    double alpha, double beta,
                                                    double* __restrict__ C, int ldc,
                                                    double* __restrict__ part) {
@@ -56,10 +71,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, int kchu
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = zero4();
+  double ra[16], rb[16];
+  if (kb < ke) {
+    stage_load<TA != 0>(ra, A, lda, i0, M, kb, ke);
+    stage_load<TBT == 0>(rb, B, ldb, j0, N, kb, ke);
+  }
   for (int k0 = kb; k0 < ke; k0 += TB) {
-    stage_g<TA != 0>(As, A, lda, i0, M, k0, ke);
-    stage_g<TBT == 0>(Bs, B, ldb, j0, N, k0, ke);
+    stage_store<TA != 0>(As, ra);
+    stage_store<TBT == 0>(Bs, rb);
     __syncthreads();
+    if (k0 + TB < ke) {          // the next K-step's operands, in flight under the MFMAs
+      stage_load<TA != 0>(ra, A, lda, i0, M, k0 + TB, ke);
+      stage_load<TBT == 0>(rb, B, ldb, j0, N, k0 + TB, ke);
+    }
 #pragma unroll 4
     for (int k4 = 0; k4 < TB / 4; ++k4) {
       const int k = k4 * 4 + lk;
@@ -262,20 +286,39 @@ extern "C" long long gp_dgemm_ws_bytes(int m, int n, int k) {
   return s > 1 ? (long long)s * m * n * 8 : 0;
 }
 
-extern "C" int gp_dgemm(int transa, int transb, int m, int n, int k, double alpha,
-                        const double* A, int lda, const double* B, int ldb, double beta,
-                        double* C, int ldc, void* ws, long long ws_bytes, hipStream_t stream) {
+template <typename EA, typename EB>
+static void launch_gemm(int transa, int transb, dim3 grid, hipStream_t stream, int m, int n,
+                        int k, int kchunk, const void* A, int lda, const void* B, int ldb,
+                        double alpha, double beta, double* C, int ldc, double* part) {
+  const EA* a = static_cast<const EA*>(A);
+  const EB* b = static_cast<const EB*>(B);
+#define GP_GEMM(TA_, TB_)                                                                     \
+  hipLaunchKernelGGL((gemm_kernel<TA_, TB_, EA, EB>), grid, dim3(256), 0, stream, m, n, k,     \
+                     kchunk, a, lda, b, ldb, alpha, beta, C, ldc, part)
+  if (transa == 0 && transb == 0) GP_GEMM(0, 0);
+  else if (transa == 0 && transb == 1) GP_GEMM(0, 1);
+  else if (transa == 1 && transb == 0) GP_GEMM(1, 0);
+  else GP_GEMM(1, 1);
+#undef GP_GEMM
+}
+
+extern "C" int gp_gemm_ex(int transa, int transb, int m, int n, int k, double alpha,
+                          const void* A, int a_f32, int lda, const void* B, int b_f32, int ldb,
+                          double beta, double* C, int ldc, void* ws, long long ws_bytes,
+                          hipStream_t stream) {
   if (transa != 0 && transa != 1) return -1;
   if (transb != 0 && transb != 1) return -2;
   if (m < 0) return -3;
   if (n < 0) return -4;
   if (k < 0) return -5;
   if (!A && k > 0) return -7;
-  if (lda < (transa ? k : m) || lda < 1) return -8;
-  if (!B && k > 0) return -9;
-  if (ldb < (transb ? n : k) || ldb < 1) return -10;
-  if (!C) return -12;
-  if (ldc < m || ldc < 1) return -13;
+  if (a_f32 != 0 && a_f32 != 1) return -8;
+  if (lda < (transa ? k : m) || lda < 1) return -9;
+  if (!B && k > 0) return -10;
+  if (b_f32 != 0 && b_f32 != 1) return -11;
+  if (ldb < (transb ? n : k) || ldb < 1) return -12;
+  if (!C) return -14;
+  if (ldc < m || ldc < 1) return -15;
   if (m == 0 || n == 0) return 0;
   int splits = (k > 0) ? choose_splits(m, n, k) : 1;
   if (splits > 1 && (!ws || ws_bytes < (long long)splits * m * n * 8)) splits = 1;
@@ -283,14 +326,18 @@ extern "C" int gp_dgemm(int transa, int transb, int m, int n, int k, double alph
   splits = (k > 0) ? gp_ceil_div(k, kchunk) : 1;
   double* part = (splits > 1) ? static_cast<double*>(ws) : nullptr;
   dim3 grid(gp_ceil_div(m, TB) * gp_ceil_div(n, TB), 1, splits);
-#define GP_GEMM(TA_, TB_)                                                                     \
-  hipLaunchKernelGGL((gemm_kernel<TA_, TB_>), grid, dim3(256), 0, stream, m, n, k, kchunk, A, \
-                     lda, B, ldb, alpha, beta, C, ldc, part)
-  if (transa == 0 && transb == 0) GP_GEMM(0, 0);
-  else if (transa == 0 && transb == 1) GP_GEMM(0, 1);
-  else if (transa == 1 && transb == 0) GP_GEMM(1, 0);
-  else GP_GEMM(1, 1);
-#undef GP_GEMM
+  if (a_f32 && b_f32)
+    launch_gemm<float, float>(transa, transb, grid, stream, m, n, k, kchunk, A, lda, B, ldb,
+                              alpha, beta, C, ldc, part);
+  else if (a_f32)
+    launch_gemm<float, double>(transa, transb, grid, stream, m, n, k, kchunk, A, lda, B, ldb,
+                               alpha, beta, C, ldc, part);
+  else if (b_f32)
+    launch_gemm<double, float>(transa, transb, grid, stream, m, n, k, kchunk, A, lda, B, ldb,
+                               alpha, beta, C, ldc, part);
+  else
+    launch_gemm<double, double>(transa, transb, grid, stream, m, n, k, kchunk, A, lda, B, ldb,
+                                alpha, beta, C, ldc, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   if (part) {
@@ -301,6 +348,16 @@ extern "C" int gp_dgemm(int transa, int transb, int m, int n, int k, double alph
     if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   }
   return 0;
+}
+
+extern "C" int gp_dgemm(int transa, int transb, int m, int n, int k, double alpha,
+                        const double* A, int lda, const double* B, int ldb, double beta,
+                        double* C, int ldc, void* ws, long long ws_bytes, hipStream_t stream) {
+  const int rc = gp_gemm_ex(transa, transb, m, n, k, alpha, A, 0, lda, B, 0, ldb, beta, C, ldc,
+                            ws, ws_bytes, stream);
+  // keep gp_dgemm's documented argument numbers (A, lda = 7, 8; B, ldb = 9, 10; C, ldc = 12, 13)
+  static const int remap[16] = {0, -1, -2, -3, -4, -5, 0, -7, 0, -8, -9, 0, -10, 0, -12, -13};
+  return (rc < 0 && rc > -16) ? remap[-rc] : rc;
 }
 
 extern "C" int gp_sim_stats(const double* Y, int n, int ny, long long ldy, double sd_floor,

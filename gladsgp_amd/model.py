@@ -47,15 +47,27 @@ def init_model(t_std, y_sim, exp, p, data_dir="data/", sd_threshold=1e-6, recomp
                device=None, float32_basis=True, omega=None, verbose=True):
     """Build EmulatorData / EmulatorModel with the PCA basis (src/model.py:20-107)."""
     y_ind_sim = np.linspace(0, 1, np.shape(y_sim)[1])
-    data = EmulatorData(t_sim=t_std, y_sim=y_sim, y_ind_sim=y_ind_sim, device=device)
-    data.standardize_y(sd_threshold=sd_threshold)           # mu, sd (ddof=1, floored), y_std
-    sd_ = data.sim_data
     os.makedirs(data_dir, exist_ok=True)
     pca_fpattern = os.path.join(data_dir, "pca_{}_{}.npy")
     have = all(os.path.exists(pca_fpattern.format(exp, a)) for a in ("U", "S", "Vh"))
+    draw = None
+    if (recompute or not have) and omega is None:
+        # randomized_svd's test matrix, np.random.normal((ny, r)) as float32 exactly as it would
+        # draw it (the same global-RNG call, nothing else draws in between), on a host thread
+        # while the ensemble is uploaded and standardised: the host draw is the PCA's largest
+        # single cost (347 of 694 ms at 512 x 1,347,945, profiles/r04/prof_pca_a.log)
+        from concurrent.futures import ThreadPoolExecutor
+        ny_, r_ = np.shape(y_sim)[1], min(PMAX, *np.shape(y_sim))
+        pool = ThreadPoolExecutor(max_workers=1)
+        draw = pool.submit(lambda: np.random.normal(size=(ny_, r_)).astype(np.float32))
+        pool.shutdown(wait=False)
+    data = EmulatorData(t_sim=t_std, y_sim=y_sim, y_ind_sim=y_ind_sim, device=device)
+    data.standardize_y(sd_threshold=sd_threshold)           # mu, sd (ddof=1, floored), y_std
+    sd_ = data.sim_data
     if recompute or not have:
         r = min(PMAX, *sd_.y_std.shape)
-        U, S, Vh = randomized_svd(sd_.y_std, r, k=0, q=1, omega=omega)
+        U, S, Vh = randomized_svd(sd_.y_std, r, k=0, q=1,
+                                  omega=draw.result() if draw is not None else omega)
         # the reference's y_std has y_sim's dtype (float32 in fit_models / load_model), and its
         # randomized_svd returns (and init_model caches) that dtype (src/svd.py:51-68,
         # model.py:87-89); the build computes in fp64 and casts the cached arrays alike

@@ -325,6 +325,16 @@ int gp_dgemm(int transa, int transb, int m, int n, int k, double alpha,
              const double* A, int lda, const double* B, int ldb, double beta,
              double* C, int ldc, void* ws, long long ws_bytes, hipStream_t stream);
 
+/* gp_dgemm with either operand stored as float32 (a_f32 / b_f32 = 1): the float32 elements are
+ * widened to fp64 as they are loaded (exactly), the products and sums are fp64, so the result
+ * is bit-identical to gp_dgemm on an fp64 copy of the operand -- from half its bytes and
+ * without the copy.  src/svd.py:51-64 receives the float32 ensemble of fit_models /
+ * load_model (src/model.py:184, 136) and multiplies it as stored; this is that product in fp64.
+ * Same workspace rule as gp_dgemm; argument numbers as listed. */
+int gp_gemm_ex(int transa, int transb, int m, int n, int k, double alpha,
+               const void* A, int a_f32, int lda, const void* B, int b_f32, int ldb,
+               double beta, double* C, int ldc, void* ws, long long ws_bytes, hipStream_t stream);
+
 /* Per-location statistics over simulations of a C-order ensemble Y (n x ny, row stride ldy):
  * mu = mean over rows, sd = std(ddof=1) floored at sd_floor — src/model.py:60-64. */
 int gp_sim_stats(const double* Y, int n, int ny, long long ldy, double sd_floor,

@@ -40,6 +40,53 @@ def test_gemm(dev, ta, tb, m, n, k):
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12 * np.sqrt(k) * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("m,n,k", [(70, 33, 129), (512, 25, 40000), (3, 200, 7)])
+def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
+    """gp_gemm_ex with a float32 A and/or B (widened on load) equals gp_gemm_ex / gp_dgemm on
+    fp64 copies of the same values bit for bit, split-K shapes included (512 x 25 x 40000 is
+    the fit's X Omega shape at a shorter field)."""
+    from gladsgp_amd.blas import CM, gemm
+    rng = np.random.default_rng(7 * m + n + k + ta * 2 + tb)
+    A = rng.standard_normal((k, m) if ta else (m, k)).astype(np.float32)
+    B = rng.standard_normal((n, k) if tb else (k, n)).astype(np.float32)
+    C0 = rng.standard_normal((m, n))
+
+    def cm(M, dt):
+        return CM(torch.as_tensor(M.T.copy(), device=dev).to(dt), M.shape[0], M.shape[1],
+                  M.shape[0])
+
+    res = {}
+    for fa, fb in ((0, 0), (1, 0), (0, 1), (1, 1)):
+        Cc = CM(_t(C0.T.copy(), dev), m, n, m)
+        gemm(bool(ta), bool(tb), cm(A, torch.float32 if fa else torch.float64),
+             cm(B, torch.float32 if fb else torch.float64), alpha=0.7, beta=-1.3, C=Cc)
+        res[(fa, fb)] = Cc.logical().cpu().numpy()
+    for key in ((1, 0), (0, 1), (1, 1)):
+        assert np.array_equal(res[key], res[(0, 0)]), key
+    ref = 0.7 * ((A.T if ta else A).astype(np.float64) @ (B.T if tb else B)) - 1.3 * C0
+    np.testing.assert_allclose(res[(0, 0)], ref, rtol=1e-12,
+                               atol=1e-12 * np.sqrt(k) * np.abs(ref).max())
+
+
+def test_randomized_svd_float32_input_reads_no_fp64_copy(dev):
+    """randomized_svd on a float32 ensemble (the reference's fit dtype) keeps it float32 on the
+    device: its outputs equal the fp64-input run's outputs cast to float32, bit for bit."""
+    from gladsgp_amd.svd import randomized_svd
+    rng = np.random.default_rng(11)
+    n, ny, r = 40, 6000, 12
+    t = rng.random((n, 3))
+    X = (np.sin(t @ rng.standard_normal((3, ny))) + 0.01 * rng.standard_normal((n, ny)))
+    X32 = X.astype(np.float32)
+    om = rng.standard_normal((ny, r)).astype(np.float32)
+    X32d = torch.as_tensor(X32, device=dev)
+    a = randomized_svd(X32d, r, k=0, q=1, omega=om)
+    b = randomized_svd(X32d.to(torch.float64), r, k=0, q=1, omega=om)
+    assert all(x.dtype == torch.float32 for x in a) and all(y.dtype == torch.float64 for y in b)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y.to(torch.float32))
+
+
 def test_sim_stats_and_standardize(dev):
     from gladsgp_amd import blas
     rng = np.random.default_rng(0)
