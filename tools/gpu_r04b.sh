@@ -32,6 +32,9 @@ cd $R
 ls gpurun_out/${TAG}_prof_nccl/
 step pptrace
 timeout -k 10 120 python tools/dbg/pp_trace.py 4096 > gpurun_out/${TAG}_pptrace.txt 2>&1 || exit 1
+step potrf_modes
+timeout -k 10 120 python tools/prof_potrf_modes.py > gpurun_out/${TAG}_potrf_modes.log 2>&1 || exit 1
+cat gpurun_out/${TAG}_potrf_modes.log
 step pca
 timeout -k 10 120 python tools/prof_pca.py > gpurun_out/${TAG}_prof_pca.log 2>&1 || exit 1
 head -3 gpurun_out/${TAG}_prof_pca.log
