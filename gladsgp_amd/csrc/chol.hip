@@ -1616,32 +1616,22 @@ GP_DEV void pp_exit(const PPArgs& P) {
   }
 }
 
-// Zero task: plain 16-B stores (read only by later launches: the kernel boundary orders them).
+// Zero task: plain stores (read only by later launches: the kernel boundary orders them).
+// Wave w takes columns w, w + 4, ...; a column's run of rows is contiguous.  Kept minimal in
+// registers: pp_kernel's allocation decides whether a cross-covariance wave still fits beside
+// it on the SIMD (tests/test_capi.py::test_persistent_factorisation_leaves_room_for_cross).
 GP_DEV void pp_zero(const PPArgs& P, const PPTask& T) {
-  double* Xb = P.X + T.b * P.sX;
+  const bool zt = T.kind == kTZ;
   const int NT = (P.N + 1) & ~1;
-  int r0, r1, c0, c1;                          // rows [64 r0, 64 r1) x columns [64 c0, 64 c1)
-  if (T.kind == kTZ) {
-    c0 = T.i; c1 = T.i + 1;
-    r0 = T.j; r1 = min(T.j + kPPZRun, T.i);
-  } else {
-    c0 = T.i; c1 = min(T.i + 8, NT);
-    r0 = P.N; r1 = NT;
-  }
-  const int rows = NB * (r1 - r0), cols = NB * (c1 - c0);
-  double* base = Xb + (long long)NB * r0 + (long long)NB * c0 * P.ldx;
-  if ((P.ldx & 1) == 0 && ((size_t)Xb & 15) == 0) {
-    const int h = rows / 2;                    // double2 per column
-    const double2 z2 = make_double2(0.0, 0.0);
-    for (int g = threadIdx.x; g < h * cols; g += 256) {
-      const int col = g / h, e = g - col * h;
-      *reinterpret_cast<double2*>(base + (long long)col * P.ldx + 2 * e) = z2;
-    }
-  } else {
-    for (int g = threadIdx.x; g < rows * cols; g += 256) {
-      const int col = g / rows, e = g - col * rows;
-      base[(long long)col * P.ldx + e] = 0.0;
-    }
+  const int c0 = T.i;
+  const int ncol = NB * (zt ? 1 : min(8, NT - c0));
+  const int r0 = zt ? T.j : P.N;
+  const int nrow = NB * (zt ? min(kPPZRun, T.i - T.j) : NT - P.N);
+  double* base = P.X + T.b * P.sX + (long long)NB * r0 + (long long)NB * c0 * P.ldx;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int col = w; col < ncol; col += 4) {
+    double* cp = base + (long long)col * P.ldx;
+    for (int e = lane; e < nrow; e += 64) cp[e] = 0.0;
   }
 }
 

@@ -186,3 +186,67 @@ def test_factorisation_workspace_entry_points(lib):
     assert lib.gp_potrf(dummy, 4, 4, 8, 2, None, None, None) == -4   # before any allocation
     assert lib.gp_loglik_status(None, 4, 1, 0, None) == -1
     assert lib.gp_loglik_status(wsp, 0, 1, 0, None) == 0
+
+
+def _kernel_resources():
+    """Per-kernel register and LDS use read from the built library's gfx950 code objects
+    (offload bundles -> AMDGPU metadata note, printed by llvm-readelf)."""
+    import re
+    import shutil
+    import struct
+    import subprocess
+    import tempfile
+    from gladsgp_amd import _build
+    readelf = shutil.which("llvm-readelf") or "/opt/rocm/llvm/bin/llvm-readelf"
+    if not os.path.exists(_build.LIB_PATH) or not os.path.exists(readelf):
+        pytest.skip("built library or llvm-readelf missing")
+    data = open(_build.LIB_PATH, "rb").read()
+    out, pos = {}, 0
+    while True:
+        i = data.find(b"__CLANG_OFFLOAD_BUNDLE__", pos)
+        if i < 0:
+            break
+        pos = i + 24
+        n = struct.unpack_from("<Q", data, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            triple = data[p:p + tl].decode(errors="replace")
+            p += tl
+            if "gfx950" not in triple or not size:
+                continue
+            with tempfile.NamedTemporaryFile(suffix=".co") as f:
+                f.write(data[i + off:i + off + size])
+                f.flush()
+                notes = subprocess.run([readelf, "--notes", f.name], capture_output=True,
+                                       text=True, check=True).stdout
+            for blk in notes.split("\n  - ")[1:]:
+                name = re.search(r"\.name:\s+(\S+)", blk)
+                if not name:
+                    continue
+                g = lambda k: int(re.search(r"\." + k + r":\s+(\d+)", blk).group(1))  # noqa
+                out[name.group(1)] = {"vgpr": g("vgpr_count"), "agpr": g("agpr_count"),
+                                      "lds": g("group_segment_fixed_size")}
+    return out
+
+
+def _alloc(r):
+    """Registers a wave of the kernel holds per lane on gfx950 (unified VGPR/AGPR file: the
+    metadata's .vgpr_count is the total, arch VGPRs + AGPRs), in granules of 8."""
+    return -(-r["vgpr"] // 8) * 8
+
+
+def test_persistent_factorisation_leaves_room_for_cross():
+    """gp_fit_predict runs the cross-covariance (cross_kp_kernel<8>, every d <= 8 config) beside
+    the persistent factorisation (pp_kernel, one 4-wave workgroup per CU); that overlap exists
+    only while one wave of each fits on a SIMD: registers <= 512 per lane, LDS <= 160 KB per CU.
+    Round 4 found it broken by 10 extra pp_kernel registers (C3 27.7 vs 26.8 ms per step: the
+    cross-covariance waited for the whole factorisation) -- this guards the budget."""
+    res = _kernel_resources()
+    pp = [v for k, v in res.items() if "pp_kernel" in k]
+    cross = [v for k, v in res.items() if "cross_kp_kernelILi8E" in k]
+    assert pp and cross, sorted(res)[:20]
+    pp, cross = pp[0], cross[0]
+    assert _alloc(pp) + _alloc(cross) <= 512, (pp, cross, _alloc(pp), _alloc(cross))
+    assert pp["lds"] + cross["lds"] <= 160 * 1024, (pp, cross)
