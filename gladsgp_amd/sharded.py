@@ -105,8 +105,9 @@ def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta,
     Returns ``(mean, var)`` of shape (m,) on rank 0 and ``None`` on the others with
     ``gather``; else this rank's block ``(mean_r, var_r, (lo, hi))``.  ``counts`` overrides the
     per-rank split (default: even for "redundant", rank 0 shortened by a measured
-    factorisation time for "broadcast" -- pass :func:`split_counts` of your own calibration to
-    avoid the measurement).  ``check`` synchronises once and raises if the factorisation
+    factorisation and prediction times for "broadcast" (:func:`calibrate_split`) -- pass
+    :func:`split_counts` / :func:`balanced_split` of your own calibration to avoid the
+    measurement).  ``check`` synchronises once and raises if the factorisation
     failed (info != 0); without it the caller owns that check.  Single process: the whole m on
     this device.
     """
@@ -122,8 +123,8 @@ def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta,
     n = X.shape[0]
     if counts is None:
         if mode == "broadcast" and dist_on:
-            t_fact, t_point = calibrate(ctx, X, Xs, beta, s, delta, s_pred, w)
-            counts = split_counts(m, world, t_fact / t_point)
+            counts, _, _ = calibrate_split(ctx, X, Xs, beta, s, delta, s_pred, w,
+                                           m_chunk=m_chunk)
         else:
             counts = [b - a for a, b in (gdist.shard_range(m, r, world) for r in range(world))]
     if len(counts) != world or sum(counts) != m:
@@ -196,6 +197,90 @@ def calibrate(ctx: gdist.Context, X, Xs, beta, s, delta, s_pred, w, points: int 
     return float(calib[0]), float(calib[1])
 
 
+def balanced_split(m: int, world: int, t_fact: float, T, granule: int = 128) -> list[int]:
+    """Test points per rank for the pipelined schedule, from measured times: rank 0 runs the
+    factorisation (``t_fact``) and predicts m0 points, ranks 1.. predict the rest split evenly;
+    m0 minimises max(t_fact + T(m0), T(m1)), m1 = ceil((m - m0) / (world - 1)).  ``T(points)``
+    is the prediction time of that many points (non-decreasing; on the GPU a staircase in the
+    TRMM's residency rounds of 32 column panels: 4096 points at n = 4096, so a point-linear
+    model misplaces the split by up to a round, ~0.9 ms of a ~3.4 ms step at 8 ranks).  m0 is
+    a multiple of ``granule`` (the TRMM's 128-point panel) or all of m."""
+    if world <= 1:
+        return [m]
+    cache = {}
+
+    def t(points):
+        if points <= 0:
+            return 0.0
+        if points not in cache:
+            cache[points] = float(T(points))
+        return cache[points]
+
+    def m1_of(m0):
+        return -(-(m - m0) // (world - 1))
+
+    # f(m0) = t_fact + T(m0) - T(m1(m0)) is non-decreasing in m0: find its sign change
+    lo, hi = 0, -(-m // world) // granule + 1          # in granules
+    if t_fact >= t(m1_of(0)):
+        best = 0
+    else:
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if t_fact + t(min(m, mid * granule)) - t(m1_of(min(m, mid * granule))) < 0:
+                lo = mid
+            else:
+                hi = mid
+        cands = {min(m, lo * granule), min(m, hi * granule)}
+        best = min(cands, key=lambda m0: (max(t_fact + t(m0), t(m1_of(m0))), -m0))
+    m0 = best
+    rest = [b - a for a, b in (gdist.shard_range(m - m0, r, world - 1) for r in range(world - 1))]
+    return [m0] + rest
+
+
+def calibrate_split(ctx: gdist.Context, X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
+                    reps: int = 3):
+    """Rank 0 measures the factorisation (Gram + gp_potrf_inv) and the prediction time of
+    candidate point counts (kernels.predict on the first points of ``Xs``, median of ``reps``)
+    and picks the split with :func:`balanced_split`; the counts are broadcast so every rank
+    uses the same.  Returns (counts, t_fact, t_point) -- t_point at a full 16384-point chunk,
+    for reporting."""
+    dev = X.device
+    world = ctx.world if ctx is not None and ctx.distributed else 1
+    m = Xs.shape[0]
+    buf = torch.zeros(world + 2, dtype=F64, device=dev)
+    if ctx is None or not ctx.distributed or ctx.rank == 0:
+        tf = []
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            ch = kernels.cholesky_inverse(kernels.gram(X, beta, s, delta))
+            torch.cuda.synchronize(dev)
+            tf.append(time.perf_counter() - t0)
+        t_fact = sorted(tf)[reps // 2]
+        ws = kernels.PredictWorkspace()
+
+        def T(points):
+            Xc = Xs[:points].contiguous()
+            kernels.predict(ch, X, Xc, beta, s, s_pred, w, m_chunk=m_chunk, workspace=ws)
+            ts = []
+            for _ in range(reps):
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                kernels.predict(ch, X, Xc, beta, s, s_pred, w, m_chunk=m_chunk, workspace=ws)
+                torch.cuda.synchronize(dev)
+                ts.append(time.perf_counter() - t0)
+            return sorted(ts)[reps // 2]
+
+        counts = balanced_split(m, world, t_fact, T)
+        mp = min(m, 16384)
+        buf[0], buf[1] = t_fact, T(mp) / mp
+        buf[2:] = torch.as_tensor(counts, dtype=F64)
+    if ctx is not None and ctx.distributed:
+        gdist.broadcast_(ctx, buf)
+    vals = buf.cpu().tolist()
+    return [int(round(v)) for v in vals[2:]], vals[0], vals[1]
+
+
 class PipelinedPredictor:
     """A stream of single-output GPs over shared (X, Xs), test points split over ranks, as a
     two-stage pipeline: ``step(params_next)`` has rank 0 factorise the next GP and broadcast its
@@ -233,9 +318,8 @@ class PipelinedPredictor:
                 if calib_gp is None:
                     raise ValueError("PipelinedPredictor: give counts or a calib_gp")
                 b, s_, d_, sp = calib_gp[:4]
-                t_fact, t_point = calibrate(ctx, self.X, Xs, b, s_, d_, sp, self.w)
-                self.t_fact, self.t_point = t_fact, t_point
-                counts = split_counts(self.m, world, t_fact / t_point)
+                counts, self.t_fact, self.t_point = calibrate_split(
+                    ctx, self.X, Xs, b, s_, d_, sp, self.w, m_chunk=m_chunk)
             else:
                 counts = [self.m]
         self.counts = counts

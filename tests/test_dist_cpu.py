@@ -190,3 +190,30 @@ def test_bench_gpus_flag_launches_ranks():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
                         "--dry-run"], capture_output=True, text=True, env=env1, timeout=200)
     assert r.returncode != 0 and "2 but 1 ranks" in r.stderr
+
+
+def test_balanced_split_minimises_the_slowest_rank():
+    """sharded.balanced_split against brute force on a staircase prediction time (the TRMM's
+    residency rounds: 4096 points per round, a partial round at 0.65 of a full one)."""
+    import math
+
+    from gladsgp_amd.sharded import balanced_split
+
+    def T(p):
+        full, part = divmod(p, 4096)
+        return 0.875e-3 * full + (0.57e-3 if part else 0.0) + 0.05e-3 * (p > 0)
+
+    for m, world, t_fact in ((100000, 8, 2.0e-3), (100000, 2, 2.0e-3), (100000, 4, 1.9e-3),
+                             (40000, 2, 0.3e-3), (5000, 8, 2.0e-3), (100000, 8, 40e-3)):
+        c = balanced_split(m, world, t_fact, T)
+        assert len(c) == world and sum(c) == m and min(c) >= 0
+        assert c[0] % 128 == 0 or c[0] == m
+        assert max(c[1:]) - min(c[1:]) <= 1
+
+        def cost(m0):
+            m1 = math.ceil((m - m0) / (world - 1))
+            return max(t_fact + T(m0), T(m1))
+
+        best = min(cost(m0) for m0 in range(0, m + 1, 128))
+        assert cost(c[0]) <= best + 1e-12, (m, world, c, cost(c[0]), best)
+    assert balanced_split(777, 1, 1.0, T) == [777]
