@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 4 follow-up job: C3 re-sweep of the cross-covariance stream's CU reservation after the
+# factorisation changes, then C4 on this box: bench, MFMA busy + effective clock (PMC), HBM
+# traffic of the TRMM (FETCH/WRITE, separate passes) -- the box-to-box spread question.
+#   tools/gpu_r04c.sh TAG
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+TAG=${1:-r04c}
+R=$(pwd)
+mkdir -p gpurun_out
+step() { echo "== $1 $(date +%T)"; }
+step sweep_aux
+FRS="0 16 32" bash tools/sweep_aux_cus.sh ${TAG}_sweep_aux > /dev/null || exit 1
+cat gpurun_out/${TAG}_sweep_aux.log
+step c4
+timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 2 > gpurun_out/${TAG}_c4.log 2>&1 || exit 1
+grep '^{' gpurun_out/${TAG}_c4.log | cut -c1-250
+step pmc_c4
+bash tools/pmc_mfma.sh c4 > gpurun_out/${TAG}_pmc_mfma_c4.txt 2>&1 || exit 1
+grep -E "trmm|cross|pp_kernel" gpurun_out/${TAG}_pmc_mfma_c4.txt
+step pmc_c3
+bash tools/pmc_mfma.sh c3 > gpurun_out/${TAG}_pmc_mfma_c3.txt 2>&1 || exit 1
+grep -E "trmm|cross|pp_kernel" gpurun_out/${TAG}_pmc_mfma_c3.txt
+step traffic_c4
+bash tools/pmc_traffic.sh c4 > gpurun_out/${TAG}_pmc_traffic_c4.txt 2>&1 || exit 1
+tail -3 gpurun_out/${TAG}_pmc_traffic_c4.txt
+step end

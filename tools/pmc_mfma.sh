@@ -1,10 +1,12 @@
 #!/bin/bash
-# MFMA busy fraction and effective clock of the C3 kernels (one --pmc pass of its own).
+# MFMA busy fraction and effective clock of the bench's kernels (one --pmc pass of its own).
+#   tools/pmc_mfma.sh [c3|c4]
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
+WL=${1:-c3}
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT -d $R/gpurun_out/pmc_mfma -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/pmc_mfma.log 2>&1 || exit 1
-timeout -k 10 120 rocprofv3 --kernel-trace -d $R/gpurun_out/pmc_mfma_kt -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/pmc_mfma_kt.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT -d $R/gpurun_out/pmc_mfma -o run --output-format csv -- python3 $R/bench.py --workload $WL --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/pmc_mfma.log 2>&1 || exit 1
+timeout -k 10 120 rocprofv3 --kernel-trace -d $R/gpurun_out/pmc_mfma_kt -o run --output-format csv -- python3 $R/bench.py --workload $WL --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/pmc_mfma_kt.log 2>&1 || exit 1
 python3 - "$R" <<'PY'
 import csv, glob, sys, collections
 R = sys.argv[1]

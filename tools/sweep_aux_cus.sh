@@ -7,7 +7,7 @@ TAG=${1:-sweep_aux_cus}
 mkdir -p gpurun_out
 : > gpurun_out/$TAG.log
 for rep in 1 2; do
-  for fr in 0 16 32 48 64; do
+  for fr in ${FRS:-0 16 32 48 64}; do
     timeout -k 10 200 python bench.py --aux-free-cus $fr --steps 10 --warmup 3 --no-cpu > gpurun_out/${TAG}_one.log 2>&1 || { cat gpurun_out/${TAG}_one.log; exit 1; }
     python -c "
 import json
