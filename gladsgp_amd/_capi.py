@@ -101,6 +101,8 @@ SIGNATURES = {
     "gp_comm_init": (c_int, [c_int, c_int, c_void_p, c_void_p]),
     "gp_comm_destroy": (c_int, [c_void_p]),
     "gp_bcast": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_void_p]),
+    "gp_pack_tril": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "gp_unpack_tril": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "gp_gather": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_void_p]),
     "gp_profile_enable": (c_int, [c_int]),
     "gp_profile_reset": (c_int, []),

@@ -150,3 +150,47 @@ extern "C" int gp_gather(void* comm, const void* send, long long bytes, void* re
   const int rc2 = rc_of(a->group_end());
   return rc ? rc : rc2;
 }
+
+// ---- Lower-triangle packing for the single-GP L^-1 broadcast (sharded.py) -------------------
+// Column c of a column-major n x n buffer, rows c .. n-1, goes to out[c n - c (c - 1) / 2 ...]:
+// n (n + 1) / 2 doubles, about half the padded square the prediction reads.  One block per
+// column, lane-consecutive 8-B accesses (a wave moves 512 contiguous bytes each way).
+namespace {
+__global__ __launch_bounds__(256) void tril_copy_kernel(const double* __restrict__ A, int n,
+                                                        long long ld, double* __restrict__ v,
+                                                        int unpack) {
+  const int c = blockIdx.x;
+  const long long off = (long long)c * n - (long long)c * (c - 1) / 2;
+  const int len = n - c;
+  double* col = const_cast<double*>(A) + (long long)c * ld + c;
+  if (!unpack) {
+    for (int e = threadIdx.x; e < len; e += 256) v[off + e] = col[e];
+  } else {
+    for (int e = threadIdx.x; e < len; e += 256) col[e] = v[off + e];
+  }
+}
+}  // namespace
+
+extern "C" int gp_pack_tril(const double* A, int n, int ld, double* out, hipStream_t stream) {
+  if (!A) return -1;
+  if (n < 0) return -2;
+  if (ld < n || ld < 1) return -3;
+  if (!out) return -4;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(tril_copy_kernel, dim3(n), dim3(256), 0, stream, A, n, (long long)ld, out,
+                     0);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+extern "C" int gp_unpack_tril(const double* in, int n, double* A, int ld, hipStream_t stream) {
+  if (!in) return -1;
+  if (n < 0) return -2;
+  if (!A) return -3;
+  if (ld < n || ld < 1) return -4;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(tril_copy_kernel, dim3(n), dim3(256), 0, stream, A, n, (long long)ld,
+                     const_cast<double*>(in), 1);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}

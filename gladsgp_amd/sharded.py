@@ -60,24 +60,33 @@ class LinvPacker:
     vector: what the broadcast carries (about half the padded square), followed by one slot
     holding the factorisation's info, so every receiver learns whether the factor it got is
     valid from the same collective (a rank-0-only raise before the broadcast would leave the
-    other ranks waiting in it)."""
+    other ranks waiting in it).  Packed and unpacked by libgpfit (gp_pack_tril /
+    gp_unpack_tril: one coalesced copy each way, no index tensor)."""
 
     def __init__(self, npad: int, device):
-        tri = torch.triu_indices(npad, npad, device=device)   # (c, r), r >= c of the [c][r] view
-        self.flat = tri[0] * npad + tri[1]
-        self.numel = int(self.flat.numel())
+        self.npad = npad
+        self.numel = npad * (npad + 1) // 2
 
     def buffer(self, device) -> torch.Tensor:
         return torch.zeros(self.numel + 1, dtype=F64, device=device)
 
+    @staticmethod
+    def order(npad: int) -> torch.Tensor:
+        """The packed layout as flat indices into the column-major (npad x npad) buffer (host
+        tensor; documents gp_pack_tril's order for host-side tests)."""
+        tri = torch.triu_indices(npad, npad)                  # (c, r), r >= c, c-major
+        return tri[0] * npad + tri[1]
+
     def pack(self, linv_buf: torch.Tensor, info: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-        torch.index_select(linv_buf.reshape(-1), 0, self.flat, out=out[: self.numel])
+        _capi.call("gp_pack_tril", linv_buf.data_ptr(), self.npad, self.npad, out.data_ptr(),
+                   kernels._stream(out.device))
         out[self.numel:].copy_(info.reshape(1).to(F64))
         return out
 
     def unpack(self, packed: torch.Tensor, linv_buf: torch.Tensor) -> torch.Tensor:
-        """Scatter into a buffer whose upper triangle and padding are already zero."""
-        linv_buf.view(-1).index_copy_(0, self.flat, packed[: self.numel])
+        """Into a buffer whose upper triangle and padding are already zero."""
+        _capi.call("gp_unpack_tril", packed.data_ptr(), self.npad, linv_buf.data_ptr(),
+                   self.npad, kernels._stream(packed.device))
         return linv_buf
 
     def info(self, packed: torch.Tensor) -> torch.Tensor:

@@ -380,6 +380,14 @@ int gp_comm_unique_id(void* id128);
 int gp_comm_init(int nranks, int rank, const void* id128, void** comm);
 int gp_comm_destroy(void* comm);
 int gp_bcast(void* comm, void* buf, long long bytes, int root, hipStream_t stream);
+
+/* Lower triangle of a column-major n x n matrix (leading dimension ld; column c from row c
+ * on) to / from a contiguous vector of n (n + 1) / 2 doubles, column after column: the payload
+ * of the single-GP L^-1 broadcast (about half the padded square the prediction reads).
+ * gp_unpack_tril writes only the lower triangle (the strict upper part of A is left as it
+ * is: zero in a buffer prepared for gp_predict). */
+int gp_pack_tril(const double* A, int n, int ld, double* out, hipStream_t stream);
+int gp_unpack_tril(const double* in, int n, double* A, int ld, hipStream_t stream);
 int gp_gather(void* comm, const void* send, long long bytes, void* recv, int root,
               hipStream_t stream);
 

@@ -144,12 +144,16 @@ def _points_worker(rank, world, port, results):
         full = torch.tril(torch.arange(1.0, npad * npad + 1, dtype=torch.float64)
                           .reshape(npad, npad)).T.contiguous().reshape(1, npad, npad)
         # together with rank 0's factorisation info, so every rank can raise alike
+        # (gp_pack_tril / gp_unpack_tril run on the GPU; here the documented layout, host-side)
         pk = LinvPacker(npad, torch.device("cpu"))
+        order = LinvPacker.order(npad)
         packed = pk.buffer(torch.device("cpu"))
         if rank == 0:
-            pk.pack(full, torch.tensor([3], dtype=torch.int32), packed)
+            packed[: pk.numel] = full.reshape(-1)[order]
+            packed[pk.numel:] = 3.0
         gdist.broadcast_(ctx, packed)
-        got = pk.unpack(packed, torch.zeros((1, npad, npad), dtype=torch.float64))
+        got = torch.zeros((1, npad, npad), dtype=torch.float64)
+        got.view(-1).index_copy_(0, order, packed[: pk.numel])
         ok_l = (bool(torch.equal(got, full)) and pk.numel == npad * (npad + 1) // 2
                 and pk.info(packed).tolist() == [3])
         results[rank] = (ok_p, ok_l)

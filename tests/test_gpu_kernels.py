@@ -528,3 +528,27 @@ def test_cholesky_grid_gram_ill_conditioned(dev, n, ell):
                                rtol=1e-10)
     Li = ch.Linv[0].cpu().numpy()
     assert np.max(np.abs(Li @ L_ref - np.eye(n))) <= 1e-16 * np.linalg.cond(G) * 100
+
+
+@pytest.mark.parametrize("n,ld", [(1, 1), (7, 9), (128, 128), (1000, 1024)])
+def test_pack_unpack_tril_round_trip(dev, n, ld):
+    """gp_pack_tril / gp_unpack_tril (the single-GP broadcast's payload): column c from row c
+    on, column after column; unpacking writes the lower triangle only."""
+    from gladsgp_amd import _capi
+    rng = np.random.default_rng(n)
+    A = rng.standard_normal((ld, n))                       # [col][row] = column-major, ld rows
+    At = torch.as_tensor(A, device=dev).contiguous()
+    v = torch.empty(n * (n + 1) // 2, dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    _capi.call("gp_pack_tril", At.data_ptr(), n, ld, v.data_ptr(), st)
+    ref = np.concatenate([A[c, c:n] for c in range(n)])
+    assert np.array_equal(v.cpu().numpy(), ref)
+    if ld == n:                                            # sharded.LinvPacker's order
+        from gladsgp_amd.sharded import LinvPacker
+        assert np.array_equal(A.reshape(-1)[LinvPacker.order(n).numpy()], ref)
+    B = torch.full((n, ld), 7.0, dtype=torch.float64, device=dev)
+    _capi.call("gp_unpack_tril", v.data_ptr(), n, B.data_ptr(), ld, st)
+    Bh = B.cpu().numpy()
+    for c in range(n):
+        assert np.array_equal(Bh[c, c:n], A[c, c:n])
+        assert np.all(Bh[c, :c] == 7.0) and np.all(Bh[c, n:] == 7.0)
