@@ -9,6 +9,12 @@ TAG=${1:-r04c}
 R=$(pwd)
 mkdir -p gpurun_out
 step() { echo "== $1 $(date +%T)"; }
+step pytest_sub
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_dist.py tests/test_gpu_rccl.py -x -v -m gpu --timeout 250 --timeout-method thread > gpurun_out/${TAG}_pytest_sub.log 2>&1
+rc=$?; tail -2 gpurun_out/${TAG}_pytest_sub.log; [ $rc -ne 0 ] && exit $rc
+step fit
+timeout -k 10 400 python bench.py --workload fit > gpurun_out/${TAG}_fit.log 2>&1 || exit 1
+grep '^{' gpurun_out/${TAG}_fit.log | cut -c1-300
 step sweep_aux
 FRS="0 16 32" bash tools/sweep_aux_cus.sh ${TAG}_sweep_aux > /dev/null || exit 1
 cat gpurun_out/${TAG}_sweep_aux.log
