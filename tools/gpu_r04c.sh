@@ -30,4 +30,7 @@ grep -E "trmm|cross|pp_kernel" gpurun_out/${TAG}_pmc_mfma_c3.txt
 step traffic_c4
 bash tools/pmc_traffic.sh c4 > gpurun_out/${TAG}_pmc_traffic_c4.txt 2>&1 || exit 1
 tail -3 gpurun_out/${TAG}_pmc_traffic_c4.txt
+step traffic_c3
+bash tools/pmc_traffic.sh c3 > gpurun_out/${TAG}_pmc_traffic_c3.txt 2>&1 || exit 1
+tail -3 gpurun_out/${TAG}_pmc_traffic_c3.txt
 step end
