@@ -343,7 +343,14 @@ class PipelinedPredictor:
         self.packed = [self.packer.buffer(self.dev) for _ in range(2)]
         # the first nonzero info among the GPs predicted so far (device; read by check())
         self.status = torch.zeros(1, dtype=torch.int32, device=self.dev)
-        self.out = torch.empty((2, max(self.ml, 1)), dtype=F64, device=self.dev)
+        # (mean, var) of this rank's block, padded to the widest block so RCCL gathers it in
+        # place into rank 0's preallocated (world, 2, mx) buffer (no per-step pad / alloc)
+        self.mx = max(max(counts), 1)
+        self.out = torch.zeros((2, self.mx), dtype=F64, device=self.dev)
+        self.gbuf = self.glist = None
+        if self.dist and ctx.backend == "nccl" and self.rank == 0:
+            self.gbuf = torch.empty((world, 2, self.mx), dtype=F64, device=self.dev)
+            self.glist = list(self.gbuf)
         self.ws = kernels.Workspace()
         self.pws = kernels.Workspace()
         self.k = 0
@@ -407,8 +414,14 @@ class PipelinedPredictor:
             kernels.predict(ch, self.X, self.Xl, b, s, sp, w, m_chunk=self.m_chunk,
                             workspace=self.ws, out=(self.out[0:1, : self.ml],
                                                     self.out[1:2, : self.ml]))
-        res = gdist.gather_cols(self.ctx, self.out[:, : self.ml], self.counts) \
-            if self.dist else self.out[:, : self.ml]
+        if not self.dist:
+            res = self.out[:, : self.ml]
+        elif self.ctx.backend == "nccl":
+            tdist.gather(self.out, gather_list=self.glist, dst=0)
+            res = torch.cat([self.gbuf[r, :, :c] for r, c in enumerate(self.counts)], dim=1) \
+                if self.rank == 0 else None
+        else:
+            res = gdist.gather_cols(self.ctx, self.out[:, : self.ml], self.counts)
         self.pending = nxt_req
         self.k = k + 1
         return res
