@@ -12,6 +12,9 @@ step() { echo "== $1 $(date +%T)"; }
 step pytest_sub
 timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_dist.py tests/test_gpu_rccl.py -x -v -m gpu --timeout 250 --timeout-method thread > gpurun_out/${TAG}_pytest_sub.log 2>&1
 rc=$?; tail -2 gpurun_out/${TAG}_pytest_sub.log; [ $rc -ne 0 ] && exit $rc
+step fact_cus
+timeout -k 10 200 python tools/prof_fact_cus.py > gpurun_out/${TAG}_fact_cus.log 2>&1 || exit 1
+cat gpurun_out/${TAG}_fact_cus.log
 step fit
 timeout -k 10 400 python bench.py --workload fit > gpurun_out/${TAG}_fit.log 2>&1 || exit 1
 grep '^{' gpurun_out/${TAG}_fit.log | cut -c1-300
