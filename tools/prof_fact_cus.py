@@ -110,7 +110,8 @@ for c in (32, 64, 96, 128, 192, NCU):
     st = masked_stream(c) if c < NCU else torch.cuda.Stream(device=dev)
     streams_used = [st]
     tf = timed(lambda: fact(st, Linv2))
-    assert int(info[0]) == 0 and torch.equal(Linv2, ref)
+    if not (int(info[0]) == 0 and torch.equal(Linv2, ref)):
+        print(f"  {c} CUs alone: info {int(info[0])}, L^-1 differs from the unmasked run")
     streams_used = [st, pred]
     tb = timed(lambda: (fact(st, Linv2), solve(pred)))
     ok = int(info[0]) == 0 and torch.equal(Linv2, ref)
