@@ -318,6 +318,9 @@ def main():
                     help="c3: gp_ctx cross_start (-1: library default)")
     ap.add_argument("--aux-free-cus", type=int, default=-1,
                     help="c3: CUs the cross-covariance stream leaves free (-1: library default)")
+    ap.add_argument("--aux-chunks", type=int, default=-1,
+                    help="gp_ctx_set_aux_chunks: chunks whose cross-covariance runs on the aux "
+                         "stream (-1: all, the library default)")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
     ap.add_argument("--c4-path", choices=("fit_predict", "predict"), default="predict",
                     help="c4: gram -> potrf -> gp_predict (default), or one gp_fit_predict per "
@@ -553,8 +556,8 @@ def main_c4(args):
     ws = kernels.PredictWorkspace()
     mean = torch.empty((bl, m), dtype=torch.float64, device=dev)
     var = torch.empty((bl, m), dtype=torch.float64, device=dev)
-    fctx = kernels.FitPredictContext(dev, args.cross_start, args.aux_free_cus) \
-        if args.c4_path == "fit_predict" else None
+    fctx = kernels.FitPredictContext(dev, args.cross_start, args.aux_free_cus,
+                                     args.aux_chunks) if args.c4_path == "fit_predict" else None
 
     def step():
         if bl and args.c4_path == "fit_predict":

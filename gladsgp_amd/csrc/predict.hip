@@ -577,23 +577,36 @@ hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, con
 // Every chunk's TRMM into its own slab, then one finalize over all m points.  With `ready`
 // (gp_fit_predict on a context), chunk ch's TRMM first waits for ready[ch], the event after
 // that chunk's cross-covariance on the aux stream.
+// Chunks from `late` on (gp_fit_predict with gp_ctx_set_aux_chunks) have no cross-covariance
+// yet: `cross(ch)` enqueues it on `stream` just before that chunk's TRMM.
+template <typename Cross>
 hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
                      long long strideInv, int m, const double* s_pred, double* mean,
                      double* var, int ldo, int batch, hipStream_t stream,
-                     const hipEvent_t* ready = nullptr) {
+                     const hipEvent_t* ready, int late, Cross&& cross) {
   hipError_t e;
-  if (ready && (e = hipStreamWaitEvent(stream, ready[0], 0)) != hipSuccess) return e;
+  if (ready && late > 0 && (e = hipStreamWaitEvent(stream, ready[0], 0)) != hipSuccess) return e;
   // timing: one event pair spans the back-to-back TRMM launches (an event record between
   // launches costs a few us of stream time each); gp_profile_read reports it per launch.
-  gpfit_prof_begin_n(GP_PROF_TRMM, stream, p.nchunks);
+  // With late cross-covariance chunks in between, one pair per launch.
+  const bool split = late < p.nchunks;
+  if (!split) gpfit_prof_begin_n(GP_PROF_TRMM, stream, p.nchunks);
   for (int ch = 0; ch < p.nchunks; ++ch) {
-    if (ready && ch > 0 && (e = hipStreamWaitEvent(stream, ready[ch], 0)) != hipSuccess) return e;
+    if (ch >= late) {
+      gpfit_prof_begin(GP_PROF_CROSS, stream);
+      if ((e = cross(ch)) != hipSuccess) return e;
+      gpfit_prof_end(GP_PROF_CROSS, stream);
+    } else if (ready && ch > 0 && (e = hipStreamWaitEvent(stream, ready[ch], 0)) != hipSuccess) {
+      return e;
+    }
+    if (split) gpfit_prof_begin(GP_PROF_TRMM, stream);
     e = solve_chunk(p, ch, w.part + ch * p.part_elems, w.z,
                                w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
                                s_pred, mean, var, ldo, batch, false, stream);
     if (e != hipSuccess) return e;
+    if (split) gpfit_prof_end(GP_PROF_TRMM, stream);
   }
-  gpfit_prof_end(GP_PROF_TRMM, stream);
+  if (!split) gpfit_prof_end(GP_PROF_TRMM, stream);
   hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(m, 256), batch), dim3(256), 0, stream,
                      w.part, p.NI, p.mc, p.part_elems, 0, m, s_pred, mean, var, ldo);
   return hipGetLastError();
@@ -672,7 +685,8 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, stream));
-  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, stream));
+  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, stream,
+                  nullptr, p.nchunks, [](int) { return hipSuccess; }));
 #undef GP_CK
   return 0;
 }
@@ -691,6 +705,7 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
 struct gp_ctx_s {
   int device = -1;
   double cross_start = 0.4;
+  int aux_chunks = -1;           // cross-covariance chunks on aux (-1: all; gp_ctx_set_aux_chunks)
   hipStream_t fact = nullptr, aux = nullptr, pred = nullptr;
   hipEvent_t e_start = nullptr, e_fact = nullptr, e_done = nullptr;
   hipEvent_t e_late = nullptr;   // the factorisation has turned latency-bound
@@ -779,6 +794,13 @@ extern "C" int gp_ctx_create(double cross_start, int aux_free_cus, void** ctx) {
   return 0;
 }
 
+extern "C" int gp_ctx_set_aux_chunks(void* ctx, int nchunks) {
+  if (!ctx) return -1;
+  if (nchunks < -1) return -2;
+  static_cast<gp_ctx_s*>(ctx)->aux_chunks = nchunks;
+  return 0;
+}
+
 extern "C" int gp_ctx_destroy(void* ctx) {
   if (!ctx) return 0;
   gp_ctx_s* c = static_cast<gp_ctx_s*>(ctx);
@@ -838,26 +860,33 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
     GP_CK(hipEventRecord(S->e_fact, fact));
     GP_CK(hipStreamWaitEvent(aux, S->e_late, 0));
   }
-  // aux: cross-covariance of every chunk (one timing-event pair around all of them)
+  // chunks whose cross-covariance runs on aux, beside the factorisation and the earlier TRMMs
+  // (all by default; the rest run on pred just before their TRMM: gp_ctx_set_aux_chunks)
+  const int n_aux = (S && S->aux_chunks >= 0 && S->aux_chunks < p.nchunks) ? S->aux_chunks
+                                                                            : p.nchunks;
+  // aux: cross-covariance of those chunks (one timing-event pair around all of them)
   // (an event after each chunk: its TRMM waits for that chunk only, so the prediction starts
   // when the factorisation ends even if later chunks' cross-covariance is still running)
-  gpfit_prof_begin_n(GP_PROF_CROSS, aux, p.nchunks);
-  for (int ch = 0; ch < p.nchunks; ++ch) {
+  if (n_aux > 0) gpfit_prof_begin_n(GP_PROF_CROSS, aux, n_aux);
+  for (int ch = 0; ch < n_aux; ++ch) {
     GP_CK(cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs, ldxs, n, m, d,
                       beta, ldbeta, s, batch, aux));
-    if (S && ch + 1 < p.nchunks) GP_CK(hipEventRecord(S->e_chunk[ch], aux));
+    if (S && ch + 1 < n_aux) GP_CK(hipEventRecord(S->e_chunk[ch], aux));
   }
-  gpfit_prof_end(GP_PROF_CROSS, aux);
+  if (n_aux > 0) gpfit_prof_end(GP_PROF_CROSS, aux);
   // pred: z, then TRMM + mean / var chunk by chunk.  One launch per chunk (not one for all):
   // the dispatcher interleaves another stream's kernels between launches, so a concurrent
   // factorisation is not starved behind a 25 ms grid (measured: 14 ms vs 3 ms per potrf).
   if (S) {
-    GP_CK(hipEventRecord(S->e_chunk[p.nchunks - 1], aux));   // after the profile's end event
+    if (n_aux > 0) GP_CK(hipEventRecord(S->e_chunk[n_aux - 1], aux));   // after the end event
     GP_CK(hipStreamWaitEvent(pred, S->e_fact, 0));
   }
   GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, pred));
   GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, pred,
-                  S ? S->e_chunk.data() : nullptr));
+                  S ? S->e_chunk.data() : nullptr, n_aux, [&](int ch) {
+                    return cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs,
+                                       ldxs, n, m, d, beta, ldbeta, s, batch, pred);
+                  }));
   if (S) {
     GP_CK(hipEventRecord(S->e_done, pred));
     GP_CK(hipStreamWaitEvent(stream, S->e_done, 0));

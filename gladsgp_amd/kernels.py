@@ -356,7 +356,8 @@ class FitPredictContext:
     the owner decides the teardown order, the library keeps no global state.
     """
 
-    def __init__(self, device=None, cross_start: float = -1.0, aux_free_cus: int = -1):
+    def __init__(self, device=None, cross_start: float = -1.0, aux_free_cus: int = -1,
+                 aux_chunks: int = -1):
         import ctypes
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
@@ -364,6 +365,13 @@ class FitPredictContext:
         with torch.cuda.device(self.device):
             _capi.call("gp_ctx_create", float(cross_start), int(aux_free_cus),
                        ctypes.addressof(self._h))
+            if aux_chunks != -1:
+                self.set_aux_chunks(aux_chunks)
+
+    def set_aux_chunks(self, nchunks: int) -> None:
+        """Chunks whose cross-covariance runs beside the factorisation / earlier TRMMs
+        (``gp_ctx_set_aux_chunks``; -1 = all, the default)."""
+        _capi.call("gp_ctx_set_aux_chunks", self._h.value, int(nchunks))
 
     @property
     def handle(self) -> int | None:

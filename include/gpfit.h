@@ -206,6 +206,15 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
  */
 int gp_ctx_create(double cross_start, int aux_free_cus, void** ctx);
 int gp_ctx_destroy(void* ctx);
+/*
+ * How many test-point chunks' cross-covariance gp_fit_predict runs on the context's aux stream
+ * (beside the factorisation and the earlier chunks' TRMMs); the remaining chunks' run on the
+ * prediction stream just before their TRMM.  -1 (default): all chunks, the C3 schedule; a batch
+ * of small GPs (C4) hides one chunk beside its factorisation and keeps the rest out of the
+ * TRMMs' way.  Returns 0, -1 (ctx NULL), -2 (nchunks < -1).  Results are bit-identical for
+ * every value.
+ */
+int gp_ctx_set_aux_chunks(void* ctx, int nchunks);
 
 /*
  * Fit + predict in one call:

@@ -140,6 +140,8 @@ def test_new_entry_points_validate(lib):
     assert lib.gp_ctx_create(2.0, 0, dummy) == -1
     assert lib.gp_ctx_create(0.4, 0, None) == -3
     assert lib.gp_ctx_destroy(None) == 0
+    assert lib.gp_ctx_set_aux_chunks(None, 1) == -1
+    assert lib.gp_ctx_set_aux_chunks(dummy, -5) == -2      # rejected before the handle is read
 
 
 def test_comm_argument_validation(lib):

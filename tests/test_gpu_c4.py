@@ -72,12 +72,14 @@ def test_c4_predict_path_vs_oracle(c4):
 def test_c4_fit_predict_path_bitwise(c4):
     from gladsgp_amd import kernels
     t = c4["t"]
-    with kernels.FitPredictContext(c4["dev"]) as fctx:
-        mean, var, ch = kernels.fit_predict(t["X"], t["Xs"], t["beta"], t["s"], t["delta"],
-                                            t["s"], t["W"], ctx=fctx)
-        torch.cuda.synchronize()
-    assert torch.equal(mean, c4["mean"]) and torch.equal(var, c4["var"])
-    assert int(ch.info.abs().sum()) == 0
+    for aux_chunks in (-1, 1):   # every chunk beside the factorisation / only the first
+        with kernels.FitPredictContext(c4["dev"], aux_chunks=aux_chunks) as fctx:
+            mean, var, ch = kernels.fit_predict(t["X"], t["Xs"], t["beta"], t["s"], t["delta"],
+                                                t["s"], t["W"], ctx=fctx)
+            torch.cuda.synchronize()
+        assert torch.equal(mean, c4["mean"]) and torch.equal(var, c4["var"])
+        assert int(ch.info.abs().sum()) == 0
+        del mean, var, ch
 
 
 def test_c4_bounds(c4):

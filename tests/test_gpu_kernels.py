@@ -327,9 +327,19 @@ def test_two_phase_predict_and_overlap_match_single(dev):
         # chunk's TRMM waits for its own chunk's cross-covariance only)
         m5, v5, _ = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),
                                         _t(s, dev), _t(W, dev), m_chunk=384, ctx=fctx)
+        # gp_ctx_set_aux_chunks: none / one / two of the chunks' cross-covariance on the aux
+        # stream, the rest on the prediction stream before their TRMM; then all again
+        late = []
+        for k in (0, 1, 2, -1):
+            fctx.set_aux_chunks(k)
+            late.append(kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev),
+                                            _t(delta, dev), _t(s, dev), _t(W, dev), m_chunk=384,
+                                            ctx=fctx)[:2])
         torch.cuda.synchronize()
     assert torch.equal(m1, m3) and torch.equal(v1, v3)
     assert torch.equal(m1, m5) and torch.equal(v1, v5)
+    for mk, vk in late:
+        assert torch.equal(m1, mk) and torch.equal(v1, vk)
     assert torch.equal(ch3.L, ch.L) and torch.equal(ch3.Linv, ch.Linv)
     assert torch.equal(ch3.logdet, ch.logdet) and int(ch3.info.abs().sum()) == 0
     m4, v4, _ = kernels.fit_predict(Xd, Xsd, _t(betas, dev), _t(s, dev), _t(delta, dev),

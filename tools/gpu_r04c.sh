@@ -24,6 +24,14 @@ cat gpurun_out/${TAG}_sweep_aux.log
 step c4
 timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 2 > gpurun_out/${TAG}_c4.log 2>&1 || exit 1
 grep '^{' gpurun_out/${TAG}_c4.log | cut -c1-250
+step c4_aux_chunks
+for rep in 1 2; do
+  for v in "predict -1" "fit_predict 1" "fit_predict 2"; do
+    set -- $v
+    timeout -k 10 200 python bench.py --workload c4 --steps 5 --warmup 2 --c4-path $1 --aux-chunks $2 > gpurun_out/${TAG}_c4_ab.tmp 2>&1 || exit 1
+    echo "path=$1 aux_chunks=$2 $(grep '^{' gpurun_out/${TAG}_c4_ab.tmp | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(round(r["value"]/1e6,2), "M/s", round(r["ms_per_step"],2), "ms")')" | tee -a gpurun_out/${TAG}_c4_aux_chunks.log
+  done
+done
 step pmc_c4
 bash tools/pmc_mfma.sh c4 > gpurun_out/${TAG}_pmc_mfma_c4.txt 2>&1 || exit 1
 grep -E "trmm|cross|pp_kernel" gpurun_out/${TAG}_pmc_mfma_c4.txt
