@@ -546,7 +546,7 @@ def test_pack_unpack_tril_round_trip(dev, n, ld):
     on, column after column; unpacking writes the lower triangle only."""
     from gladsgp_amd import _capi
     rng = np.random.default_rng(n)
-    A = rng.standard_normal((ld, n))                       # [col][row] = column-major, ld rows
+    A = rng.standard_normal((n, ld))                       # [col][row] = column-major, ld rows
     At = torch.as_tensor(A, device=dev).contiguous()
     v = torch.empty(n * (n + 1) // 2, dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
