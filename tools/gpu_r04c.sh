@@ -21,6 +21,9 @@ grep '^{' gpurun_out/${TAG}_fit.log | cut -c1-300
 step sweep_aux
 FRS="0 16 32" bash tools/sweep_aux_cus.sh ${TAG}_sweep_aux > /dev/null || exit 1
 cat gpurun_out/${TAG}_sweep_aux.log
+step sweep_cross_start
+FRS="0" CSS="0 0.2 0.6" bash tools/sweep_aux_cus.sh ${TAG}_sweep_cs > /dev/null || exit 1
+cat gpurun_out/${TAG}_sweep_cs.log
 step c4
 timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 2 > gpurun_out/${TAG}_c4.log 2>&1 || exit 1
 grep '^{' gpurun_out/${TAG}_c4.log | cut -c1-250
