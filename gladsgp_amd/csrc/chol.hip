@@ -1385,7 +1385,21 @@ GP_DEV double* pp_dptr(const PPArgs& P, int b, int j, int& ld) {
   return Xb + (long long)j * NB * NB;
 }
 
-GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
+// The persistent kernel's two task families are calls, not inlined into its dispatch loop:
+// inlined, their register allocations added up (chain alone 344 VGPRs+AGPRs, workers alone 350,
+// both 462), and a kernel at 462 leaves room for one 48-register cross-covariance wave per SIMD
+// beside it; as calls the kernel takes 353 (+176 B of scratch per lane for the call frames),
+// which leaves room for three.
+#ifndef PP_TASK_CALLS
+#define PP_TASK_CALLS 1
+#endif
+#if PP_TASK_CALLS
+#define PP_TASK __device__ __attribute__((noinline))
+#else
+#define PP_TASK GP_DEV
+#endif
+
+PP_TASK void pp_worker(const PPArgs& P, const PPTask& T) {
   Smem& sm = g_sm;
   const int N = P.N;
   int* F = P.flags + (long long)T.b * P.fstride;
@@ -1481,7 +1495,7 @@ GP_DEV void pp_worker(const PPArgs& P, const PPTask& T) {
 }
 
 // The chain of problem b (see the section comment).
-GP_DEV void pp_chain(const PPArgs& P, int b) {
+PP_TASK void pp_chain(const PPArgs& P, int b) {
   Smem& sm = g_sm;
   const int N = P.N;
   int* F = P.flags + (long long)b * P.fstride;
