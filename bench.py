@@ -318,14 +318,15 @@ def main():
                     help="c3: gp_ctx cross_start (-1: library default)")
     ap.add_argument("--aux-free-cus", type=int, default=-1,
                     help="c3: CUs the cross-covariance stream leaves free (-1: library default)")
-    ap.add_argument("--aux-chunks", type=int, default=-1,
+    ap.add_argument("--aux-chunks", type=int, default=None,
                     help="gp_ctx_set_aux_chunks: chunks whose cross-covariance runs on the aux "
-                         "stream (-1: all, the library default)")
+                         "stream (-1: all; default: all for c3, 2 for c4)")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
-    ap.add_argument("--c4-path", choices=("fit_predict", "predict"), default="predict",
-                    help="c4: gram -> potrf -> gp_predict (default), or one gp_fit_predict per "
-                         "step (measured 1-3%% slower at C4: its cross-covariance, 5x the "
-                         "batched potrf, stretches the potrf and the TRMM waits for all of it)")
+    ap.add_argument("--c4-path", choices=("fit_predict", "predict"), default="fit_predict",
+                    help="c4: one gp_fit_predict per step with the first --aux-chunks chunks' "
+                         "cross-covariance beside the batched factorisation (default; 60.08-"
+                         "60.55 vs 60.67-61.13 ms/step, profiles/r04/r04d_c4_aux_chunks.log), "
+                         "or gram -> potrf -> gp_predict")
     args = ap.parse_args()
     rc = launch_ranks(args)
     if rc is not None:
@@ -358,8 +359,8 @@ def main():
     bd = torch.as_tensor(beta, device=dev).reshape(1, d)
     sd = torch.tensor([s], dtype=torch.float64, device=dev)
     dd = torch.tensor([delta], dtype=torch.float64, device=dev)
-    fctx = None if args.serial else kernels.FitPredictContext(dev, args.cross_start,
-                                                              args.aux_free_cus)
+    fctx = None if args.serial else kernels.FitPredictContext(
+        dev, args.cross_start, args.aux_free_cus, -1 if args.aux_chunks is None else args.aux_chunks)
     ws = kernels.PredictWorkspace()
     out = torch.empty((2, ml), dtype=torch.float64, device=dev)   # rows: mean, var
 
@@ -556,8 +557,9 @@ def main_c4(args):
     ws = kernels.PredictWorkspace()
     mean = torch.empty((bl, m), dtype=torch.float64, device=dev)
     var = torch.empty((bl, m), dtype=torch.float64, device=dev)
+    aux_chunks = 2 if args.aux_chunks is None else args.aux_chunks
     fctx = kernels.FitPredictContext(dev, args.cross_start, args.aux_free_cus,
-                                     args.aux_chunks) if args.c4_path == "fit_predict" else None
+                                     aux_chunks) if args.c4_path == "fit_predict" else None
 
     def step():
         if bl and args.c4_path == "fit_predict":
@@ -621,7 +623,8 @@ def main_c4(args):
                    "parallelism": f"PC shards x{ctx.world} (RCCL broadcast + gather)",
                    "collectives": (f"{ctx.backend} process group of {ctx.world}"
                                    if ctx.distributed else "none (single process)"),
-                   "path": args.c4_path},
+                   "path": args.c4_path,
+                   "aux_chunks": aux_chunks if args.c4_path == "fit_predict" else None},
         "roofline": {"kernel": "trmm_pair_kernel (rank 0's PCs)", "bound": "mfma",
                      "achieved": round(tr_tfs, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),

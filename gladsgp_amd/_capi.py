@@ -71,6 +71,8 @@ SIGNATURES = {
     "gp_ctx_create": (c_int, [ctypes.c_double, c_int, c_void_p]),
     "gp_ctx_destroy": (c_int, [c_void_p]),
     "gp_ctx_set_aux_chunks": (c_int, [c_void_p, c_int]),
+    "gp_host_legacy_normal_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll,
+                                          c_void_p, c_int]),
     "gp_loglik_ws_bytes": (c_ll, [c_int, c_int]),
     "gp_loglik": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                           c_void_p, c_int, c_int, c_void_p, c_ll, c_void_p, c_void_p,

@@ -1385,13 +1385,15 @@ GP_DEV double* pp_dptr(const PPArgs& P, int b, int j, int& ld) {
   return Xb + (long long)j * NB * NB;
 }
 
-// The persistent kernel's two task families are calls, not inlined into its dispatch loop:
-// inlined, their register allocations added up (chain alone 344 VGPRs+AGPRs, workers alone 350,
-// both 462), and a kernel at 462 leaves room for one 48-register cross-covariance wave per SIMD
-// beside it; as calls the kernel takes 353 (+176 B of scratch per lane for the call frames),
-// which leaves room for three.
+// The persistent kernel's two task families are inlined into its dispatch loop, where their
+// register allocations add up (chain alone 344 VGPRs+AGPRs, workers alone 350, both 462: room
+// for one 48-register cross-covariance wave per SIMD beside it).  As calls (PP_TASK_CALLS=1)
+// the kernel takes 353 (+176 B of scratch per lane for the call frames), room for three; the
+// cross-covariance then ran 1.09 instead of ~2 ms per C3 step, but the factorisation took 2.17
+// instead of 1.81 ms alone and 2.40 beside it, and the C3 step got slower (27.05-27.21 ms,
+// profiles/r04/r04d_*; same-box A/B in r04e_*).
 #ifndef PP_TASK_CALLS
-#define PP_TASK_CALLS 1
+#define PP_TASK_CALLS 0
 #endif
 #if PP_TASK_CALLS
 #define PP_TASK __device__ __attribute__((noinline))

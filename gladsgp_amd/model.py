@@ -24,7 +24,7 @@ from . import blas
 from .blas import CM, gemm
 from .emulator import EmulatorData, EmulatorModel
 from .mcmc import SepiaParam
-from .svd import randomized_svd
+from .svd import legacy_normal_f32, randomized_svd
 
 PMAX = 25   # model.py:81
 
@@ -53,13 +53,14 @@ def init_model(t_std, y_sim, exp, p, data_dir="data/", sd_threshold=1e-6, recomp
     draw = None
     if (recompute or not have) and omega is None:
         # randomized_svd's test matrix, np.random.normal((ny, r)) as float32 exactly as it would
-        # draw it (the same global-RNG call, nothing else draws in between), on a host thread
-        # while the ensemble is uploaded and standardised: the host draw is the PCA's largest
-        # single cost (347 of 694 ms at 512 x 1,347,945, profiles/r04/prof_pca_a.log)
+        # draw it (the same global-RNG stream, nothing else draws in between), on a host thread
+        # while the ensemble is uploaded and standardised: numpy's own draw was the PCA's largest
+        # single cost (347 of 694 ms at 512 x 1,347,945, profiles/r04/prof_pca_a.log), hence
+        # svd.legacy_normal_f32 (bit-identical, vectorised + threaded host generator)
         from concurrent.futures import ThreadPoolExecutor
         ny_, r_ = np.shape(y_sim)[1], min(PMAX, *np.shape(y_sim))
         pool = ThreadPoolExecutor(max_workers=1)
-        draw = pool.submit(lambda: np.random.normal(size=(ny_, r_)).astype(np.float32))
+        draw = pool.submit(legacy_normal_f32, (ny_, r_))
         pool.shutdown(wait=False)
     data = EmulatorData(t_sim=t_std, y_sim=y_sim, y_ind_sim=y_ind_sim, device=device)
     data.standardize_y(sd_threshold=sd_threshold)           # mu, sd (ddof=1, floored), y_std

@@ -28,10 +28,12 @@ is read (src/svd.py:66-76): mirrored.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
-from . import kernels
+from . import _capi, kernels
 from .blas import CM, gemm, rowscale, shift_diag, syevj
 
 _U = 2.0 ** -53
@@ -109,6 +111,31 @@ def _orthonormalize_deficient(Y: CM, rel_tol: float = 1e-10, seed: int = 0x5EED)
     return Q
 
 
+def legacy_normal_f32(shape, threads: int | None = None) -> np.ndarray:
+    """``np.random.normal(size=shape).astype(np.float32)`` on numpy's global legacy generator,
+    bit for bit (``src/svd.py:51``), drawn by libgpfit's host generator
+    (``gp_host_legacy_normal_f32``: vectorised MT19937, the polar method's log / sqrt on
+    ``threads`` host threads); numpy's global state is advanced exactly as that call would."""
+    import os
+    name, key, pos, has_gauss, cached = np.random.get_state()
+    if name != "MT19937":
+        raise ValueError(f"legacy_normal_f32: global generator is {name}, not MT19937")
+    if threads is None:
+        env = os.environ.get("OMP_NUM_THREADS")
+        threads = int(env) if env and env.isdigit() and int(env) > 0 else \
+            len(os.sched_getaffinity(0))
+        threads = min(threads, 16)
+    out = np.empty(shape, dtype=np.float32)
+    key = np.array(key, dtype=np.uint32, copy=True)
+    pos_c, hg_c, g_c = ctypes.c_int(int(pos)), ctypes.c_int(int(has_gauss)), \
+        ctypes.c_double(float(cached))
+    _capi.call("gp_host_legacy_normal_f32", key.ctypes.data, ctypes.addressof(pos_c),
+               ctypes.addressof(hg_c), ctypes.addressof(g_c), int(out.size), out.ctypes.data,
+               int(threads))
+    np.random.set_state(("MT19937", key, pos_c.value, hg_c.value, g_c.value))
+    return out
+
+
 def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=None):
     """Same signature and return shapes as ``src/svd.py:randomized_svd``.
 
@@ -133,7 +160,7 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
     if r > 1024:
         raise ValueError("randomized_svd: p + k must be <= 1024 (Jacobi core)")
     if omega is None:
-        omega = np.random.normal(size=(n_cols, r)).astype(np.float32)
+        omega = legacy_normal_f32((n_cols, r))
     Om = _to_device(omega, dev).contiguous()      # float32 (as drawn) or float64
     Xc = CM.of_rowmajor(Xt)          # (n_cols x m_rows), ld = n_cols
     Oc = CM.of_rowmajor(Om)          # (r x n_cols)

@@ -312,6 +312,19 @@ int gp_mcmc_group_decide(const gp_mcmc_state* S, const int* kinds, int g, int la
                          const double* ll_all, hipStream_t stream);
 
 /*
+ * Host-side (no device, no stream): `count` float32 deviates of numpy's legacy global
+ * generator exactly as src/svd.py:51 draws randomized_svd's test matrix,
+ * np.random.normal(size=...).astype(np.float32) -- MT19937 + the polar Box-Muller method
+ * (numpy's legacy_gauss), bit-identical -- continued from and advancing the caller's state:
+ * key[624] / pos (np.random.get_state()[1:3]) and the cached deviate has_gauss / gauss
+ * ([3:5]).  Twist and candidate tests vectorised, the accepted pairs' log / sqrt on `nthreads`
+ * host threads.  Returns 0, -1 (a state pointer NULL), -2 (pos outside [0, 624]), -5 (count < 0),
+ * -6 (out NULL).
+ */
+int gp_host_legacy_normal_f32(unsigned int* key, int* pos, int* has_gauss, double* gauss,
+                              long long count, float* out, int nthreads);
+
+/*
  * One marginal realisation per entry: out[i] = mean[i] + sqrt(max(var[i], 0)) z_i, z_i ~ N(0,1)
  * from counter-based Philox4x32-10 keyed by `seed` (counter (i/2, offset); Box-Muller pairs),
  * so the draws depend only on (seed, offset, i).  out may alias mean.  The opt-in realize mode

@@ -8,6 +8,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -252,3 +253,37 @@ def test_persistent_factorisation_leaves_room_for_cross():
     pp, cross = pp[0], cross[0]
     assert _alloc(pp) + _alloc(cross) <= 512, (pp, cross, _alloc(pp), _alloc(cross))
     assert pp["lds"] + cross["lds"] <= 160 * 1024, (pp, cross)
+
+
+@pytest.mark.parametrize("seed,pre,shape", [
+    (0, 0, (1,)), (0, 1, (1,)), (1, 0, (2,)), (2, 3, (3,)), (3, 0, (7, 5)), (4, 5, (1000,)),
+    (5, 0, (624,)), (6, 623, (20001,)), (7, 0, (3000, 50)), (8, 311, (157,)), (9, 2, (0,))])
+def test_legacy_normal_matches_numpy(seed, pre, shape):
+    """svd.legacy_normal_f32 (gp_host_legacy_normal_f32, host code: no GPU) == the reference's
+    np.random.normal(size=...).astype(np.float32) (src/svd.py:51) bit for bit, from any
+    generator position (pre draws: odd counts leave a cached deviate, pos anywhere in a twist),
+    and numpy's global state afterwards equals the state numpy's own call leaves."""
+    from gladsgp_amd.svd import legacy_normal_f32
+    np.random.seed(seed)
+    np.random.normal(size=pre)
+    st = np.random.get_state()
+    ref = np.random.normal(size=shape).astype(np.float32)
+    st_ref = np.random.get_state()
+    np.random.set_state(st)
+    got = legacy_normal_f32(shape, threads=3)
+    st_got = np.random.get_state()
+    assert got.dtype == np.float32 and got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(st_got[1], st_ref[1]) and st_got[2:] == st_ref[2:]
+
+
+def test_legacy_normal_argument_validation(lib):
+    key = (ctypes.c_uint * 624)()
+    pos, hg, g = ctypes.c_int(624), ctypes.c_int(0), ctypes.c_double(0.0)
+    out = (ctypes.c_float * 4)()
+    f = lib.gp_host_legacy_normal_f32
+    assert f(None, ctypes.byref(pos), ctypes.byref(hg), ctypes.byref(g), 4, out, 1) == -1
+    bad = ctypes.c_int(625)
+    assert f(key, ctypes.byref(bad), ctypes.byref(hg), ctypes.byref(g), 4, out, 1) == -2
+    assert f(key, ctypes.byref(pos), ctypes.byref(hg), ctypes.byref(g), -1, out, 1) == -5
+    assert f(key, ctypes.byref(pos), ctypes.byref(hg), ctypes.byref(g), 4, None, 1) == -6

@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p _ab
 objs=""
-for f in gram predict linalg profile blas eig comm rng mcmc; do objs="$objs gladsgp_amd/_obj/$f.o"; done
+for f in gram predict linalg profile blas eig comm rng mcmc host_rng; do objs="$objs gladsgp_amd/_obj/$f.o"; done
 pids=""
 for spec in "$@"; do
   name=${spec%%:*}; src=${spec#*:}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4: the persistent factorisation with its task families as calls (353 registers, room for
-# three cross-covariance waves per SIMD) against the inlined form (462, room for one):
+# three cross-covariance waves per SIMD) against the inlined default (462, room for one):
 # correctness of the new default, then same-box A/B of the factorisation alone, the C3 / C4
 # benches and the fit.
 #   tools/gpu_r04e.sh TAG      (needs _ab/libgpfit_calls.so, _ab/libgpfit_inline.so)
@@ -21,4 +21,7 @@ cat gpurun_out/${TAG}_ab_bench.log
 step ab_fit
 bash tools/ab_fit_libs.sh ${TAG}_ab_fit _ab/libgpfit_calls.so _ab/libgpfit_inline.so > /dev/null || exit 1
 cat gpurun_out/${TAG}_ab_fit.log
+step pca
+timeout -k 10 300 python tools/prof_pca.py > gpurun_out/${TAG}_prof_pca.log 2>&1 || exit 1
+tail -15 gpurun_out/${TAG}_prof_pca.log
 step end
