@@ -56,7 +56,9 @@ def gemm_ev(transa, transb, A, B, alpha=1.0, beta=0.0, C=None):
     nn = B.rows if transb else B.cols
     gemms.append({"op": f"gemm({int(transa)},{int(transb)}) {m}x{nn}x{k}",
                   "ms": e0.elapsed_time(e1),
-                  "bytes": 8.0 * (m * k + k * nn + m * nn)})
+                  # operand bytes as stored: gp_gemm_ex reads float32 operands as float32
+                  "bytes": (4.0 if A.f32 else 8.0) * m * k + (4.0 if B.f32 else 8.0) * k * nn
+                  + 8.0 * m * nn})
     return out
 
 
