@@ -120,16 +120,19 @@ void transform(const double* xy, long long p0, long long p1, long long pair0, fl
   }
 }
 
-}  // namespace
+// Worker threads joined on every exit path (a joinable std::thread must not be destroyed).
+struct Joiner {
+  std::vector<std::thread> t;
+  void join() {
+    for (auto& x : t)
+      if (x.joinable()) x.join();
+    t.clear();
+  }
+  ~Joiner() { join(); }
+};
 
-extern "C" int gp_host_legacy_normal_f32(unsigned int* key, int* pos, int* has_gauss, double* gauss,
-                                         long long count, float* out, int nthreads) {
-  if (!key || !pos || !has_gauss || !gauss) return -1;
-  if (*pos < 0 || *pos > kMtN) return -2;
-  if (count < 0) return -5;
-  if (count > 0 && !out) return -6;
-  if (count == 0) return 0;
-  if (nthreads < 1) nthreads = 1;
+int legacy_normal_impl(uint32_t* key, int* pos, int* has_gauss, double* gauss, long long count,
+                       float* out, int nthreads) {
   const bool avx2 = __builtin_cpu_supports("avx2");
   auto twist = avx2 ? twist_temper_avx2 : twist_temper_base;
   auto accept = avx2 ? accept_avx2 : accept_base;
@@ -152,11 +155,8 @@ extern "C" int gp_host_legacy_normal_f32(unsigned int* key, int* pos, int* has_g
   constexpr long long kBatch = 1 << 20;                 // pairs per batch (16 MB)
   std::vector<double> xy[2] = {std::vector<double>(2 * (kBatch + kMtN)),
                                std::vector<double>(2 * (kBatch + kMtN))};
-  std::vector<std::thread> pool;
-  auto join = [&] {
-    for (auto& t : pool) t.join();
-    pool.clear();
-  };
+  Joiner pool;
+  auto join = [&] { pool.join(); };
   long long done = 0;          // pairs handed to the transform
   int cur = 0;
   long long fill = 0;          // pairs in xy[cur]
@@ -170,7 +170,7 @@ extern "C" int gp_host_legacy_normal_f32(unsigned int* key, int* pos, int* has_g
     const int T = (int)std::min<long long>(nthreads, std::max<long long>(1, n / 4096));
     for (int t = 0; t < T; ++t) {
       const long long a = n * t / T, b = n * (t + 1) / T;
-      pool.emplace_back(transform, src, a, b, pair0, out, base, count);
+      pool.t.emplace_back(transform, src, a, b, pair0, out, base, count);
     }
     done += n;
     fill = 0;
@@ -223,4 +223,21 @@ extern "C" int gp_host_legacy_normal_f32(unsigned int* key, int* pos, int* has_g
     *gauss = f * last_x1;
   }
   return 0;
+}
+
+}  // namespace
+
+extern "C" int gp_host_legacy_normal_f32(unsigned int* key, int* pos, int* has_gauss, double* gauss,
+                                         long long count, float* out, int nthreads) {
+  if (!key || !pos || !has_gauss || !gauss) return -1;
+  if (*pos < 0 || *pos > kMtN) return -2;
+  if (count < 0) return -5;
+  if (count > 0 && !out) return -6;
+  if (count == 0) return 0;
+  if (nthreads < 1) nthreads = 1;
+  try {
+    return legacy_normal_impl(key, pos, has_gauss, gauss, count, out, nthreads);
+  } catch (...) {   // thread or buffer allocation failed: nothing escapes the C ABI
+    return -7;
+  }
 }

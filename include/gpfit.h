@@ -319,7 +319,8 @@ int gp_mcmc_group_decide(const gp_mcmc_state* S, const int* kinds, int g, int la
  * key[624] / pos (np.random.get_state()[1:3]) and the cached deviate has_gauss / gauss
  * ([3:5]).  Twist and candidate tests vectorised, the accepted pairs' log / sqrt on `nthreads`
  * host threads.  Returns 0, -1 (a state pointer NULL), -2 (pos outside [0, 624]), -5 (count < 0),
- * -6 (out NULL).
+ * -6 (out NULL), -7 (a host thread or buffer could not be created; the state is then
+ * undefined: restore it from a copy).
  */
 int gp_host_legacy_normal_f32(unsigned int* key, int* pos, int* has_gauss, double* gauss,
                               long long count, float* out, int nthreads);
