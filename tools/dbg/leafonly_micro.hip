@@ -1,0 +1,57 @@
+// Microbenchmark (debug only): cycles of one 16 x 16 leaf (leaf16 = one MFMA per column,
+// leaf16b = blocked with LDS shuffles, leaf16c = blocked lane-local) on wave 0 of one
+// workgroup, and of diag_factor_blk's non-leaf work for comparison.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form \
+//     -Xclang -target-feature -Xclang +enable-ds128 tools/dbg/leafonly_micro.hip -o ...
+#include "../../gladsgp_amd/csrc/chol.hip"
+#include <cstdio>
+#include <vector>
+
+template <int V>
+__global__ __launch_bounds__(256, 1) void probe(const double* G, long long* out) {
+  LdsSmem& sm = *(LdsSmem*)&g_sm;
+  for (int rep = 0; rep < 4; ++rep) {
+    for (int g = threadIdx.x; g < NB * NB; g += 256) sm.As[(g >> 6) * LP + (g & 63)] = G[g];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const long long t0 = __builtin_amdgcn_s_memtime();
+      if (V == 0) leaf16(sm.As, sm.Bs, 0, sm.invs);
+      else if (V == 1) leaf16b(sm.As, sm.Bs, 0, sm.invs);
+      else leaf16c(sm.As, sm.Bs, 0, sm.invs);
+      __builtin_amdgcn_s_waitcnt(0);
+      const long long t1 = __builtin_amdgcn_s_memtime();
+      if (threadIdx.x == 0) out[V * 4 + rep] = t1 - t0;
+    }
+    __syncthreads();
+  }
+}
+
+int main() {
+  double* dG; long long* dout;
+  (void)hipMalloc(&dG, NB * NB * 8); (void)hipMalloc(&dout, 16 * 8);
+  std::vector<double> G(NB * NB);
+  for (int i = 0; i < NB; ++i)
+    for (int j = 0; j < NB; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < 8; ++k) {
+        const double xi = ((i * 37 + k * 11) % 64) / 64.0, xj = ((j * 37 + k * 11) % 64) / 64.0;
+        s += (xi - xj) * (xi - xj);
+      }
+      G[i * NB + j] = exp(-s) + (i == j ? 1e-3 : 0.0);
+    }
+  (void)hipMemcpy(dG, G.data(), G.size() * 8, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(probe<0>, dim3(1), dim3(256), 0, 0, dG, dout);
+  hipLaunchKernelGGL(probe<1>, dim3(1), dim3(256), 0, 0, dG, dout);
+  hipLaunchKernelGGL(probe<2>, dim3(1), dim3(256), 0, 0, dG, dout);
+  std::vector<long long> o(16);
+  (void)hipMemcpy(o.data(), dout, 16 * 8, hipMemcpyDeviceToHost);
+  const char* nm[3] = {"leaf16 (MFMA per column)", "leaf16b (blocked, LDS shuffles)",
+                       "leaf16c (blocked, lane-local)"};
+  for (int v = 0; v < 3; ++v)
+    printf("%-34s %lld %lld %lld %lld cycles\n", nm[v], o[v * 4], o[v * 4 + 1], o[v * 4 + 2],
+           o[v * 4 + 3]);
+  return 0;
+}
+extern "C" int gp_padded_n(int n) { return n <= 0 ? 0 : gp_ceil_div(n, GPFIT_TILE) * GPFIT_TILE; }
+void gpfit_prof_begin(int, hipStream_t) {}
+void gpfit_prof_end(int, hipStream_t) {}
