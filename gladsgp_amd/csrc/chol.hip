@@ -443,115 +443,24 @@ GP_DEV void leaf16(lds_double* T, lds_double* U, int o, lds_double* piv) {
 }
 
 #ifndef PP_LEAF_BLOCKED
-#define PP_LEAF_BLOCKED 0   // 1: leaf16b (permlane broadcasts), 2: leaf16b with LDS shuffles
+#define PP_LEAF_BLOCKED 1   // 0: leaf16 (one MFMA per column), 1: leaf16_blocked
 #endif
 
-// Blocked leaf (PP_LEAF_BLOCKED): the same elimination four columns at a time.  Within block q
-// (columns 4q .. 4q+3, whose rows are register q: lane 16k + c = row 4q + k, column c) the
-// block's own rows are eliminated by VALU row operations -- row j reaches the block's other row
-// groups by a lane shuffle, its multiplier A[j][i] / p_j by a second one -- and then ONE MFMA
-// applies the block's rank-4 update to every later row (A operand: lane 16k + i holds
-// M[i][4q+k] = A[4q+k][i] / p_{4q+k} for i > 4q+3; B operand: the block's rows themselves,
-// masked to c > 4q + k), and one more to W.  Both factors still come from row j only.  The
-// per-column dependent chain is readlane -> rcp + 2 Newton -> multiply -> FMA, the MFMA's
-// latency paid once per four columns instead of once per column.
-// Row jj (lanes 16 jj .. 16 jj + 15) of x broadcast to all four rows of the wave: gfx950's
-// v_permlane16_swap (odd rows <-> even rows of the partner register) then v_permlane32_swap
-// (upper half <-> lower half), two VALU ops per 32-bit half instead of an LDS-path shuffle.
-template <int JJ>
-GP_DEV double row_bcast(double x) {
-  const unsigned long long u = __double_as_longlong(x);
-  unsigned h[2] = {(unsigned)u, (unsigned)(u >> 32)};
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const auto s16 = __builtin_amdgcn_permlane16_swap(h[e], h[e], false, false);
-    const unsigned a = (JJ & 1) ? s16[1] : s16[0];      // rows (jj&1, jj&1, 2+(jj&1), 2+(jj&1))
-    const auto s32 = __builtin_amdgcn_permlane32_swap(a, a, false, false);
-    h[e] = (JJ & 2) ? s32[1] : s32[0];                  // row jj everywhere
-  }
-  return __longlong_as_double(((unsigned long long)h[1] << 32) | h[0]);
-}
-
-GP_DEV void leaf16b(lds_double* T, lds_double* U, int o, lds_double* piv) {
-  const int lane = threadIdx.x & 63;
-  const int r0 = lane >> 4, c = lane & 15;
-  f64x4 A = ld16(T + o * LP + o);
-  f64x4 W;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) W[q] = (r0 + 4 * q == c) ? 1.0 : 0.0;
-  double colpiv = 1.0;          // p_c of this lane's column
-  double rowpiv[4];             // p_r of rows r0 + 4q
-#pragma unroll
-  for (int q = 0; q < 4; ++q) rowpiv[q] = 1.0;
-  static_for<0, 4, 1>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    double rp_row = 1.0;        // 1 / p of this lane's row of block q (row 4q + r0)
-    static_for<0, 4, 1>([&](auto JJ) {
-      constexpr int jj = decltype(JJ)::value;
-      constexpr int j = 4 * q + jj;
-      const double p = readlane_f64(A[q], 16 * jj + j);
-      colpiv = (c == j) ? p : colpiv;
-      rowpiv[q] = (r0 == jj) ? p : rowpiv[q];
-      if constexpr (j < 15) {
-        const double rp = rcp_nr(p);
-        rp_row = (r0 == jj) ? rp : rp_row;
-        if constexpr (jj < 3) {
-#ifndef LEAF_RJ
-#define LEAF_RJ 0
-#endif
-#ifndef LEAF_AJ
-#define LEAF_AJ 0
-#endif
-#ifndef LEAF_WJ
-#define LEAF_WJ 0
-#endif
-          double rj, wj, aj = 0.0;
-          if constexpr (LEAF_RJ == 1) rj = row_bcast<jj>(A[q]);      // A[j][c]
-          else rj = __shfl(A[q], 16 * jj + c);
-          if constexpr (LEAF_WJ == 1) wj = row_bcast<jj>(W[q]);      // W[j][c]
-          else wj = __shfl(W[q], 16 * jj + c);
-          if constexpr (LEAF_AJ == 1) {                               // A[j][4q + r0]
-            static_for<jj + 1, 4, 1>([&](auto K) {
-              constexpr int k = decltype(K)::value;
-              const double v = readlane_f64(A[q], 16 * jj + 4 * q + k);
-              aj = (r0 == k) ? v : aj;
-            });
-          } else {
-            aj = __shfl(A[q], 16 * jj + 4 * q + r0);
-          }
-          const double m = aj * rp;
-          const bool rows = r0 > jj;
-          A[q] = (rows && c > j) ? fma(-m, rj, A[q]) : A[q];
-          W[q] = rows ? fma(-m, wj, W[q]) : W[q];
-        }
-      }
-    });
-    if constexpr (q < 3) {
-      const double row = A[q];
-      const double a = (c > 4 * q + 3) ? -(row * rp_row) : 0.0;
-      const double b = (c > 4 * q + r0) ? row : 0.0;
-      const double wq = W[q];
-      A = mfma16x16x4(a, b, A);
-      W = mfma16x16x4(a, wq, W);
-    }
-  });
-  const double rsc = rsqrt_nr(colpiv);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = r0 + 4 * q;
-    const double rsr = rsqrt_nr(rowpiv[q]);
-    T[(o + r) * LP + o + c] = r >= c ? A[q] * rsc : 0.0;
-    U[(o + r) * LP + o + c] = r >= c ? W[q] * rsr : 0.0;
-  }
-  if (lane < 16) piv[o + c] = colpiv;
-}
-
-// Blocked leaf, lane-local form (PP_LEAF_BLOCKED == 3): at the start of block q every row group
-// receives all four of the block's rows (four row broadcasts, one LDS-path round for A and one
-// for W), so lane 16k + c holds A[4q..4q+3][c]; the block's four elimination steps are then
-// lane-local FMAs whose multipliers A[j][4q+k] / p_j are wave-uniform (readlanes), and each lane
-// takes its own row back for the trailing MFMA.  Same arithmetic as leaf16b.
-GP_DEV void leaf16c(lds_double* T, lds_double* U, int o, lds_double* piv) {
+// Blocked leaf (PP_LEAF_BLOCKED, the default): the same elimination four columns at a time.
+// At the start of block q (columns 4q .. 4q+3, whose rows are register q: lane 16k + c = row
+// 4q + k, column c) every row group receives all four of the block's rows (four lane shuffles
+// for A, four for W), so lane 16k + c holds A[4q..4q+3][c]; the block's four elimination steps
+// are then lane-local FMAs whose multipliers A[j][4q+k] / p_j are wave-uniform (readlanes of
+// row j), and each lane takes its own row back.  ONE MFMA then applies the block's rank-4 update
+// to every later row (A operand: lane 16k + i holds -M[i][4q+k] = -A[4q+k][i] / p_{4q+k} for
+// i > 4q+3; B operand: the block's rows, masked to c > 4q + k), and one more to W.  Both
+// factors still come from row j only.  The MFMA's latency is paid once per four columns instead
+// of once per column: 4.08k vs 5.11k cycles per leaf, 23.4k vs 28.0k per 64 x 64 factor
+// (tools/dbg/leafonly_micro.hip, diag_micro.hip); gp_potrf_inv n = 4096 1.813 -> 1.728 ms,
+// 1024 x 32 0.997 -> 0.955, 2048 x 4 1.036 -> 0.988, fit 1.49-1.56 -> 1.45-1.47 ms per sweep
+// (profiles/r04/r04f_*).  Broadcasting row j per step instead (LDS shuffles: 23.6k; gfx950's
+// v_permlane16/32_swap: 28.4k) was no faster.
+GP_DEV void leaf16_blocked(lds_double* T, lds_double* U, int o, lds_double* piv) {
   const int lane = threadIdx.x & 63;
   const int r0 = lane >> 4, c = lane & 15;
   f64x4 A = ld16(T + o * LP + o);
@@ -640,8 +549,7 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
     // rows <= b-1, the final L_{b-1,k}, the rows above -- are all complete), which the serial
     // phase after the last leaf used to do
     if (w == 0) {
-      if constexpr (PP_LEAF_BLOCKED == 3) leaf16c(T, U, 16 * b, piv);
-      else if constexpr (PP_LEAF_BLOCKED) leaf16b(T, U, 16 * b, piv);
+      if constexpr (PP_LEAF_BLOCKED) leaf16_blocked(T, U, 16 * b, piv);
       else leaf16(T, U, 16 * b, piv);
     }
     else if (b >= 2 && w <= b - 1) inv_block(b - 1, w - 1);

@@ -1,6 +1,5 @@
 // Microbenchmark (debug only): cycles of one 16 x 16 leaf (leaf16 = one MFMA per column,
-// leaf16b = blocked with LDS shuffles, leaf16c = blocked lane-local) on wave 0 of one
-// workgroup, and of diag_factor_blk's non-leaf work for comparison.
+// leaf16_blocked = four columns per MFMA update, lane-local) on wave 0 of one workgroup.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form \
 //     -Xclang -target-feature -Xclang +enable-ds128 tools/dbg/leafonly_micro.hip -o ...
 #include "../../gladsgp_amd/csrc/chol.hip"
@@ -16,8 +15,7 @@ __global__ __launch_bounds__(256, 1) void probe(const double* G, long long* out)
     if (threadIdx.x < 64) {
       const long long t0 = __builtin_amdgcn_s_memtime();
       if (V == 0) leaf16(sm.As, sm.Bs, 0, sm.invs);
-      else if (V == 1) leaf16b(sm.As, sm.Bs, 0, sm.invs);
-      else leaf16c(sm.As, sm.Bs, 0, sm.invs);
+      else leaf16_blocked(sm.As, sm.Bs, 0, sm.invs);
       __builtin_amdgcn_s_waitcnt(0);
       const long long t1 = __builtin_amdgcn_s_memtime();
       if (threadIdx.x == 0) out[V * 4 + rep] = t1 - t0;
@@ -42,12 +40,10 @@ int main() {
   (void)hipMemcpy(dG, G.data(), G.size() * 8, hipMemcpyHostToDevice);
   hipLaunchKernelGGL(probe<0>, dim3(1), dim3(256), 0, 0, dG, dout);
   hipLaunchKernelGGL(probe<1>, dim3(1), dim3(256), 0, 0, dG, dout);
-  hipLaunchKernelGGL(probe<2>, dim3(1), dim3(256), 0, 0, dG, dout);
   std::vector<long long> o(16);
   (void)hipMemcpy(o.data(), dout, 16 * 8, hipMemcpyDeviceToHost);
-  const char* nm[3] = {"leaf16 (MFMA per column)", "leaf16b (blocked, LDS shuffles)",
-                       "leaf16c (blocked, lane-local)"};
-  for (int v = 0; v < 3; ++v)
+  const char* nm[2] = {"leaf16 (MFMA per column)", "leaf16_blocked"};
+  for (int v = 0; v < 2; ++v)
     printf("%-34s %lld %lld %lld %lld cycles\n", nm[v], o[v * 4], o[v * 4 + 1], o[v * 4 + 2],
            o[v * 4 + 3]);
   return 0;
