@@ -459,7 +459,8 @@ GP_DEV void leaf16(lds_double* T, lds_double* U, int o, lds_double* piv) {
 // (tools/dbg/leafonly_micro.hip, diag_micro.hip); gp_potrf_inv n = 4096 1.813 -> 1.728 ms,
 // 1024 x 32 0.997 -> 0.955, 2048 x 4 1.036 -> 0.988, fit 1.49-1.56 -> 1.45-1.47 ms per sweep
 // (profiles/r04/r04f_*).  Broadcasting row j per step instead (LDS shuffles: 23.6k; gfx950's
-// v_permlane16/32_swap: 28.4k) was no faster.
+// v_permlane16/32_swap: 28.4k) was no faster, nor was replaying W on wave 3 (idle during the
+// leaves) from multipliers handed over through LDS per block: 28.0k.
 GP_DEV void leaf16_blocked(lds_double* T, lds_double* U, int o, lds_double* piv) {
   const int lane = threadIdx.x & 63;
   const int r0 = lane >> 4, c = lane & 15;
