@@ -22,6 +22,9 @@ grep '^{' gpurun_out/${TAG}_bench.log | cut -c1-300
 step c4
 timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 2 > gpurun_out/${TAG}_c4.log 2>&1 || exit 1
 grep '^{' gpurun_out/${TAG}_c4.log | cut -c1-250
+step fit
+timeout -k 10 300 python bench.py --workload fit > gpurun_out/${TAG}_fit.log 2>&1 || exit 1
+grep '^{' gpurun_out/${TAG}_fit.log | cut -c1-250
 step rocprof_c3
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_prof -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu > $R/gpurun_out/${TAG}_prof.log 2>&1 || exit 1
