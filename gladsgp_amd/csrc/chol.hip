@@ -488,7 +488,16 @@ GP_DEV void leaf16_blocked(lds_double* T, lds_double* U, int o, lds_double* piv)
       colpiv = (c == j) ? p : colpiv;
       rowpiv[q] = (r0 == jj) ? p : rowpiv[q];
       if constexpr (j < 15) {
-        const double rp = rcp_nr(p);
+        // 1 / p_j: v_rcp_f64's estimate (~2^-26: 1e-8 residuals alone) + one Newton step, as
+        // accurate as two here (|LL^T - G| and |L^-1 L - I| unchanged on the micro-benchmark's
+        // tiles) and one dependent FMA pair shorter: 22.7k vs 23.4k cycles per 64 x 64 factor
+        // (profiles/r04/leaf_micro_nr*.log)
+#ifndef LEAF_NR
+#define LEAF_NR 1
+#endif
+        double rp = __builtin_amdgcn_rcp(p);
+        if constexpr (LEAF_NR >= 1) rp = fma(rp, fma(-p, rp, 1.0), rp);
+        if constexpr (LEAF_NR >= 2) rp = fma(rp, fma(-p, rp, 1.0), rp);
         rpk[jj] = rp;
         static_for<jj + 1, 4, 1>([&](auto K) {
           constexpr int k = decltype(K)::value;
