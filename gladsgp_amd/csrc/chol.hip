@@ -563,6 +563,17 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
       else leaf16(T, U, 16 * b, piv);
     }
     else if (b >= 2 && w <= b - 1) inv_block(b - 1, w - 1);
+    else if (b == 3 && w == 3) {
+      // the last row's sums over the rows already final (k = c .. 1), beside leaf 3, into the
+      // blocks the last-row pass continues from (the same MFMA accumulation order: bit-identical)
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        f64x4 acc = zero4();
+        for (int k = c2; k < 2; ++k)
+          mm16(acc, T + 16 * 3 * LP + 16 * k, LP, 1, U + 16 * k * LP + 16 * c2, LP, 1, false);
+        st16(T + 16 * c2 * LP + 16 * 3, acc, 1.0);
+      }
+    }
     __syncthreads();
     if constexpr (b < 3) {
       // panel: L_rb = A_rb Dinv_b^T, r = b + w
@@ -604,7 +615,17 @@ GP_DEV int diag_factor_blk(int nb, double* ld_out) {
       sm.red[0] = l;
     }
   }
-  if (w < 3) inv_block(3, w);   // the last row of the inverse (rows 1, 2: beside the leaves)
+  if (w < 3) {
+    // the last row of the inverse (rows 1, 2: beside the leaves; this row's k < 2 terms too)
+    lds_double* tmp = T + 16 * w * LP + 16 * 3;
+    f64x4 acc = (w < 2) ? ld16(tmp) : zero4();
+    mm16(acc, T + 16 * 3 * LP + 16 * 2, LP, 1, U + 16 * 2 * LP + 16 * w, LP, 1, false);
+    st16(tmp, acc, 1.0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    f64x4 x = zero4();
+    mm16(x, U + 16 * 3 * LP + 16 * 3, LP, 1, tmp, LP, 1, false);
+    st16(U + 16 * 3 * LP + 16 * w, x, -1.0);
+  }
   __syncthreads();
   // zero the strict upper blocks of L^-1 (the chain's GEMM and the D_j store read the whole
   // tile; L's upper blocks are never read: it is stored lower-only, then overwritten)
