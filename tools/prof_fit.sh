@@ -20,9 +20,13 @@ for s, e, _ in ev:
         cur_e = max(cur_e, e)
 busy += cur_e - cur_s
 print(f"kernels {len(ev)}, span {(t1-t0)/1e6:.1f} ms, busy {busy/1e6:.1f} ms ({100*busy/(t1-t0):.0f}%)")
+import re
+def key(n):
+    n = re.sub(r"^void ", "", n.replace("(anonymous namespace)::", ""))
+    return n.split("(")[0][:60]
 agg = collections.defaultdict(lambda: [0, 0])
 for s, e, n in ev:
-    k = n.split("(")[0][-60:]
+    k = key(n)
     agg[k][0] += 1; agg[k][1] += e - s
 for k, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:15]:
     print(f"{k:60s} {c:7d} {t/1e6:9.1f} ms  {t/c/1e3:8.1f} us")
