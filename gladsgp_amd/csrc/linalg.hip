@@ -48,13 +48,16 @@ __global__ __launch_bounds__(1024) void trmv_kernel(const double* __restrict__ L
 // out[b] = sign * (1/2 ||z_b||^2 + 1/2 logdet[b]); a problem whose matrix is not positive
 // definite (info[b] > 0, when info is given) gets sign * +inf, a factorisation that gave up
 // (info[b] < 0, an internal error) NaN and raises the sticky `status` word (when given).
+// info_out (when given) receives info[b]: gp_loglik's caller copy without a separate memcpy
+// (one hipMemcpyAsync per Metropolis group before, ~5 us each).
 __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restrict__ z, int ldz,
                                                          int n,
                                                          const double* __restrict__ logdet,
                                                          const int* __restrict__ info,
                                                          double sign,
                                                          double* __restrict__ nll,
-                                                         int* __restrict__ status) {
+                                                         int* __restrict__ status,
+                                                         int* __restrict__ info_out) {
   const int b = blockIdx.x;
   const double* zb = z + (long long)b * ldz;
   double acc = 0.0;
@@ -68,6 +71,7 @@ __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restric
     const double v = 0.5 * ((red[0] + red[1]) + (red[2] + red[3])) + 0.5 * logdet[b];
     const int f = info ? info[b] : 0;
     nll[b] = f < 0 ? __builtin_nan("") : sign * (f > 0 ? __builtin_huge_val() : v);
+    if (info_out) info_out[b] = f;
     if (f < 0 && status)
       __hip_atomic_fetch_or(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -124,7 +128,7 @@ extern "C" int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
   hipError_t e = gpfit_trmv_launch(Linv, ldinv, strideInv, w, ldw, work, n, n, n, batch, stream);
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   hipLaunchKernelGGL(nll_reduce_kernel, dim3(batch), dim3(256), 0, stream, work, n, n, logdet,
-                     (const int*)nullptr, 1.0, nll, (int*)nullptr);
+                     (const int*)nullptr, 1.0, nll, (int*)nullptr, (int*)nullptr);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }
@@ -204,13 +208,9 @@ extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* b
                                    batch, stream);
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   hipLaunchKernelGGL(nll_reduce_kernel, dim3(batch), dim3(256), 0, stream, c.z, n, n, c.logdet,
-                     (const int*)c.info, -1.0, ll, c.status);
+                     (const int*)c.info, -1.0, ll, c.status, info);
   e = hipGetLastError();
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
-  if (info) {
-    e = hipMemcpyAsync(info, c.info, sizeof(int) * batch, hipMemcpyDeviceToDevice, stream);
-    if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
-  }
   return 0;
 }
 
