@@ -287,3 +287,16 @@ def test_legacy_normal_argument_validation(lib):
     assert f(key, ctypes.byref(bad), ctypes.byref(hg), ctypes.byref(g), 4, out, 1) == -2
     assert f(key, ctypes.byref(pos), ctypes.byref(hg), ctypes.byref(g), -1, out, 1) == -5
     assert f(key, ctypes.byref(pos), ctypes.byref(hg), ctypes.byref(g), 4, None, 1) == -6
+
+
+def test_legacy_normal_reproduces_the_reference_omega():
+    """The golden test matrices drawn by the reference's own src/svd.py:51 after
+    np.random.seed(123) (tests/golden/svd_ref_64x500.npz, make_golden.py) come out of
+    svd.legacy_normal_f32 bit for bit after the same seed."""
+    from gladsgp_amd.svd import legacy_normal_f32
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "svd_ref_64x500.npz"))
+    for tag in ("p8", "p25k0"):
+        ref = g[f"{tag}_omega"]
+        np.random.seed(123)
+        got = legacy_normal_f32(ref.shape, threads=4)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), tag
