@@ -62,6 +62,14 @@ def init_from_env(device_type: str | None = None, backend: str | None = None,
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if "MASTER_PORT" not in os.environ:
+                if world > 1:
+                    # every rank picking its own free port would leave rank 0 listening on one
+                    # port and the others dialling others until the rendezvous times out
+                    raise RuntimeError(
+                        f"init_from_env: WORLD_SIZE={world} but MASTER_PORT is not set; launch "
+                        "with torchrun / torch.distributed.run or export MASTER_PORT on every "
+                        "rank")
+                # the one-rank rehearsal (force_group): nobody else has to find this port
                 os.environ["MASTER_PORT"] = str(_free_port())
             kw = {"device_id": device} if backend == "nccl" else {}
             dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)

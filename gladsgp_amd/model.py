@@ -24,7 +24,7 @@ from . import blas
 from .blas import CM, gemm
 from .emulator import EmulatorData, EmulatorModel
 from .mcmc import SepiaParam
-from .svd import legacy_normal_f32, randomized_svd
+from .svd import LegacyNormalDraw, randomized_svd
 
 PMAX = 25   # model.py:81
 
@@ -52,23 +52,27 @@ def init_model(t_std, y_sim, exp, p, data_dir="data/", sd_threshold=1e-6, recomp
     have = all(os.path.exists(pca_fpattern.format(exp, a)) for a in ("U", "S", "Vh"))
     draw = None
     if (recompute or not have) and omega is None:
-        # randomized_svd's test matrix, np.random.normal((ny, r)) as float32 exactly as it would
-        # draw it (the same global-RNG stream, nothing else draws in between), on a host thread
-        # while the ensemble is uploaded and standardised: numpy's own draw was the PCA's largest
-        # single cost (347 of 694 ms at 512 x 1,347,945, profiles/r04/prof_pca_a.log), hence
-        # svd.legacy_normal_f32 (bit-identical, vectorised + threaded host generator)
-        from concurrent.futures import ThreadPoolExecutor
-        ny_, r_ = np.shape(y_sim)[1], min(PMAX, *np.shape(y_sim))
-        pool = ThreadPoolExecutor(max_workers=1)
-        draw = pool.submit(legacy_normal_f32, (ny_, r_))
-        pool.shutdown(wait=False)
+        # randomized_svd's test matrix as the reference draws it in init_model's
+        # randomized_svd(y_std, 25, k=0) (src/svd.py:51, model.py:84): np.random.normal((ny, 25))
+        # as float32, whatever n -- the same global-RNG stream and the same advance of it --
+        # on a host thread while the ensemble is uploaded and standardised: numpy's own draw was
+        # the PCA's largest single cost (347 of 694 ms at 512 x 1,347,945,
+        # profiles/r04/prof_pca_a.log), hence the bit-identical vectorised + threaded host
+        # generator.  numpy's state is read here and advanced at draw.result(), both on this
+        # thread (svd.LegacyNormalDraw).
+        draw = LegacyNormalDraw((np.shape(y_sim)[1], PMAX))
     data = EmulatorData(t_sim=t_std, y_sim=y_sim, y_ind_sim=y_ind_sim, device=device)
     data.standardize_y(sd_threshold=sd_threshold)           # mu, sd (ddof=1, floored), y_std
     sd_ = data.sim_data
     if recompute or not have:
+        # fewer than 25 runs (or nodes): range(X Omega) is already all of range(X) with
+        # min(n, ny) test vectors, so the first r columns of the reference's Omega give its
+        # U, S, Vh (up to signs and rounding) without a rank-deficient B B^T
         r = min(PMAX, *sd_.y_std.shape)
-        U, S, Vh = randomized_svd(sd_.y_std, r, k=0, q=1,
-                                  omega=draw.result() if draw is not None else omega)
+        om = draw.result() if draw is not None else omega
+        if draw is not None and r < PMAX:
+            om = np.ascontiguousarray(om[:, :r])
+        U, S, Vh = randomized_svd(sd_.y_std, r, k=0, q=1, omega=om)
         # the reference's y_std has y_sim's dtype (float32 in fit_models / load_model), and its
         # randomized_svd returns (and init_model caches) that dtype (src/svd.py:51-68,
         # model.py:87-89); the build computes in fp64 and casts the cached arrays alike

@@ -252,10 +252,21 @@ def calibrate_split(ctx: gdist.Context, X, Xs, beta, s, delta, s_pred, w, m_chun
     candidate point counts (kernels.predict on the first points of ``Xs``, median of ``reps``)
     and picks the split with :func:`balanced_split`; the counts are broadcast so every rank
     uses the same.  Returns (counts, t_fact, t_point) -- t_point at a full 16384-point chunk,
-    for reporting."""
+    for reporting.  One rank: ([m], nan, nan) with nothing measured.  The result is memoised
+    per (device, n, m, world, m_chunk), so one-shot :func:`predict_sharded` callers pay the
+    measurement once per shape (pass ``counts`` to skip it entirely)."""
     dev = X.device
     world = ctx.world if ctx is not None and ctx.distributed else 1
     m = Xs.shape[0]
+    key = (str(dev), X.shape[0], m, world, int(m_chunk))
+    if world == 1:
+        # one rank: the split is [m] whatever the times (a one-rank communicator rehearsal
+        # included); nothing to measure
+        return [m], float("nan"), float("nan")
+    if key in _SPLIT_CACHE:
+        # the split depends on the shapes, not on the GP's values: measured once per shape
+        # (every rank holds the same cache entry, so no collective is needed)
+        return _SPLIT_CACHE[key]
     buf = torch.zeros(world + 2, dtype=F64, device=dev)
     if ctx is None or not ctx.distributed or ctx.rank == 0:
         tf = []
@@ -287,7 +298,14 @@ def calibrate_split(ctx: gdist.Context, X, Xs, beta, s, delta, s_pred, w, m_chun
     if ctx is not None and ctx.distributed:
         gdist.broadcast_(ctx, buf)
     vals = buf.cpu().tolist()
-    return [int(round(v)) for v in vals[2:]], vals[0], vals[1]
+    res = ([int(round(v)) for v in vals[2:]], vals[0], vals[1])
+    _SPLIT_CACHE[key] = res
+    return res
+
+
+# calibrate_split's results per (device, n, m, world, m_chunk): one-shot predict_sharded callers
+# pay the measurement once per shape, not on every call
+_SPLIT_CACHE: dict = {}
 
 
 class PipelinedPredictor:

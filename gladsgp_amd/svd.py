@@ -116,8 +116,16 @@ def legacy_normal_f32(shape, threads: int | None = None) -> np.ndarray:
     bit for bit (``src/svd.py:51``), drawn by libgpfit's host generator
     (``gp_host_legacy_normal_f32``: vectorised MT19937, the polar method's log / sqrt on
     ``threads`` host threads); numpy's global state is advanced exactly as that call would."""
+    out, state = _legacy_normal_from(np.random.get_state(), shape, threads)
+    np.random.set_state(state)
+    return out
+
+
+def _legacy_normal_from(state, shape, threads: int | None = None):
+    """The draw of :func:`legacy_normal_f32` from an explicit numpy state tuple, touching no
+    global state: returns (deviates, the state numpy's own call would leave)."""
     import os
-    name, key, pos, has_gauss, cached = np.random.get_state()
+    name, key, pos, has_gauss, cached = state[:5]
     if name != "MT19937":
         raise ValueError(f"legacy_normal_f32: global generator is {name}, not MT19937")
     if threads is None:
@@ -132,8 +140,31 @@ def legacy_normal_f32(shape, threads: int | None = None) -> np.ndarray:
     _capi.call("gp_host_legacy_normal_f32", key.ctypes.data, ctypes.addressof(pos_c),
                ctypes.addressof(hg_c), ctypes.addressof(g_c), int(out.size), out.ctypes.data,
                int(threads))
-    np.random.set_state(("MT19937", key, pos_c.value, hg_c.value, g_c.value))
-    return out
+    return out, ("MT19937", key, pos_c.value, hg_c.value, g_c.value)
+
+
+class LegacyNormalDraw:
+    """:func:`legacy_normal_f32` on a host worker thread.  numpy's global state is read here, on
+    the calling thread, and set to the advanced state by :meth:`result`, on the calling thread
+    again: the worker runs only the C generator on its own copy of the state, so it never reads
+    or writes numpy's global generator (a main-thread draw in between would see the state before
+    this draw, as if it had come first, and :meth:`result` then overwrites its advance)."""
+
+    def __init__(self, shape, threads: int | None = None):
+        from concurrent.futures import ThreadPoolExecutor
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise ValueError(f"legacy_normal_f32: global generator is {st[0]}, not MT19937")
+        pool = ThreadPoolExecutor(max_workers=1)
+        self._fut = pool.submit(_legacy_normal_from, st, shape, threads)
+        pool.shutdown(wait=False)
+        self._out = None
+
+    def result(self) -> np.ndarray:
+        if self._out is None:
+            self._out, state = self._fut.result()
+            np.random.set_state(state)
+        return self._out
 
 
 def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=None):

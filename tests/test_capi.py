@@ -257,7 +257,11 @@ def test_persistent_factorisation_leaves_room_for_cross():
 
 @pytest.mark.parametrize("seed,pre,shape", [
     (0, 0, (1,)), (0, 1, (1,)), (1, 0, (2,)), (2, 3, (3,)), (3, 0, (7, 5)), (4, 5, (1000,)),
-    (5, 0, (624,)), (6, 623, (20001,)), (7, 0, (3000, 50)), (8, 311, (157,)), (9, 2, (0,))])
+    (5, 0, (624,)), (6, 623, (20001,)), (7, 0, (3000, 50)), (8, 311, (157,)), (9, 2, (0,)),
+    # above 2 x kBatch (2^20 accepted pairs = 2^21 deviates per batch, host_rng.hip): the
+    # double-buffered path -- flush(false), buffer swap, one batch's transform threads beside
+    # the next batch's fill -- runs several times, as it does for the fit's 1.35M x 25 Omega
+    (10, 7, (4_300_001,))])
 def test_legacy_normal_matches_numpy(seed, pre, shape):
     """svd.legacy_normal_f32 (gp_host_legacy_normal_f32, host code: no GPU) == the reference's
     np.random.normal(size=...).astype(np.float32) (src/svd.py:51) bit for bit, from any
@@ -275,6 +279,25 @@ def test_legacy_normal_matches_numpy(seed, pre, shape):
     assert got.dtype == np.float32 and got.shape == ref.shape
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert np.array_equal(st_got[1], st_ref[1]) and st_got[2:] == st_ref[2:]
+
+
+def test_legacy_normal_draw_on_worker_thread():
+    """svd.LegacyNormalDraw (init_model's Omega, drawn beside the upload): the same deviates as
+    the reference's np.random.normal((ny, 25)).astype(float32) (src/svd.py:51), numpy's global
+    state read on the calling thread when the draw starts and advanced there by result()."""
+    from gladsgp_amd.svd import LegacyNormalDraw
+    np.random.seed(11)
+    st0 = np.random.get_state()
+    ref = np.random.normal(size=(30001, 25)).astype(np.float32)
+    st_ref = np.random.get_state()
+    np.random.set_state(st0)
+    draw = LegacyNormalDraw((30001, 25), threads=2)
+    got = draw.result()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    st = np.random.get_state()
+    assert np.array_equal(st[1], st_ref[1]) and st[2:] == st_ref[2:]
+    assert draw.result() is got                 # result() advances the state once
+    assert np.array_equal(np.random.get_state()[1], st_ref[1])
 
 
 def test_legacy_normal_argument_validation(lib):

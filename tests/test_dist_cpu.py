@@ -221,3 +221,15 @@ def test_balanced_split_minimises_the_slowest_rank():
         best = min(cost(m0) for m0 in range(0, m + 1, 128))
         assert cost(c[0]) <= best + 1e-12, (m, world, c, cost(c[0]), best)
     assert balanced_split(777, 1, 1.0, T) == [777]
+
+
+def test_init_from_env_multi_rank_needs_master_port(monkeypatch):
+    """WORLD_SIZE > 1 without MASTER_PORT fails at once (each rank picking its own free port
+    would hang the rendezvous); only the one-rank force_group rehearsal picks a port itself."""
+    from gladsgp_amd import dist as gdist
+    for k in ("MASTER_PORT", "MASTER_ADDR"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    with pytest.raises(RuntimeError, match="MASTER_PORT"):
+        gdist.init_from_env("cpu", backend="gloo")

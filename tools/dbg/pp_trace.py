@@ -15,8 +15,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from gladsgp_amd import _build, _capi  # noqa: E402
 
-if not os.path.exists(_build.TRACE_LIB_PATH):
-    sys.exit(f"{_build.TRACE_LIB_PATH} missing: python -m gladsgp_amd._build --trace")
+if (not os.path.exists(_build.TRACE_LIB_PATH) or
+        os.path.getmtime(_build.TRACE_LIB_PATH) < os.path.getmtime(_build.LIB_PATH)):
+    # missing, or older than the shipped library (whose ABI _capi binds in full: a stale trace
+    # build lacking a newer symbol would fail the bind); rebuild (stale objects only)
+    print("rebuilding", _build.build_library(trace=True), file=sys.stderr)
 _capi.LIB_PATH = _build.TRACE_LIB_PATH        # this process only: the diagnostics variant
 from gladsgp_amd import kernels  # noqa: E402
 

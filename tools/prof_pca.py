@@ -66,8 +66,8 @@ def gemm_ev(transa, transb, A, B, alpha=1.0, beta=0.0, C=None):
 emulator.SimData.__init__ = timed("upload (H2D + widen to fp64)", emulator.SimData.__init__)
 emulator.EmulatorData.standardize_y = timed("standardise (gp_sim_stats + gp_standardize)",
                                             emulator.EmulatorData.standardize_y)
-gmodel.legacy_normal_f32 = timed("Omega draw (svd.legacy_normal_f32, host thread)",
-                                 gsvd.legacy_normal_f32)
+gsvd._legacy_normal_from = timed("Omega draw (svd.LegacyNormalDraw, host thread)",
+                                 gsvd._legacy_normal_from)
 gsvd.gemm = gemm_ev
 gsvd.orthonormalize = timed("CholeskyQR3 (orthonormalize)", gsvd.orthonormalize)
 gsvd.syevj = timed("Jacobi eig of B B^T (gp_syevj)", gsvd.syevj)
