@@ -22,6 +22,7 @@
 #include "gpfit_profile.h"
 #include "gpfit_internal.h"
 #include "../../include/gpfit.h"
+#include <atomic>
 #include <new>
 #include <vector>
 
@@ -149,16 +150,71 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
 #define TRMM_XCD_PANELS 8
 #endif
 constexpr int kXcdPanels = TRMM_XCD_PANELS;
-GP_DEV void trmm_block_tile(int bid, int NI, int NC, int& p, int& C) {
-  const int NP = (NI + 1) / 2;
-  if (kXcdPanels > 0 && NC % (8 * kXcdPanels) == 0) {
-    const int x = bid & 7, t = bid >> 3, per = kXcdPanels * NP;
-    const int grp = t / per, j = t - grp * per;
-    p = j / kXcdPanels;
-    C = x + 8 * (grp * kXcdPanels + j % kXcdPanels);
+
+// One TRMM launch covers `NCt` column panels of each of `batch` problems -- the panels of one
+// test-point chunk, or of the last two chunks merged (a chunk whose blocks fill less than one
+// residency round runs with the chunk before it, trmm_launch) -- numbered g = b * NCt + C
+// (problem-major).  Panel C of the launch lies in chunk C / NCc (relative to the launch's first
+// chunk), whose cross-covariance and partial sums are `slab` / `pslab` doubles after the first
+// chunk's.
+//
+// The schedule (which blocks compute which tiles, trmm_sched) changes no sum: every tile (I, g)
+// is computed by one block with the same K order wherever it runs (natural order, or for a tile
+// that is the second of its row-tile pair, its diagonal block first: trmm_diag_first), so
+// results are bit-identical whatever the chunking and the schedule.
+struct TrmmArgs {
+  const double* Linv;
+  long long sL;
+  const double* Kt2;       // the launch's first chunk's cross-covariance slab
+  long long sK, slab;      // problem stride inside a slab; slab stride (chunk to chunk)
+  const double* z;
+  double* part;            // the launch's first chunk's partial-sum slab
+  long long pslab;         // partial-sum slab stride
+  int ld, mc, NCc, NCt, npad, NI;
+  int Gp;                  // panels g < Gp: row-tile pair blocks (uniform 8 (NI + 1) K steps)
+  int Gx;                  //   ... of which g < Gx (a multiple of 8 kXcdPanels) in the XCD order
+  int Qc;                  // panels g >= Gp: one block per tile, longest tiles first
+};
+
+// A tile's K order: the second tile of a row-tile pair (I < NI - 1 - I) runs its diagonal block
+// first (kDiagFirst, below); every other tile runs k = 0, 1, ... .
+GP_DEV bool trmm_diag_first(int I, int NI);
+
+// blockIdx.x -> (panel g, first tile I0, second tile I1 or -1).
+//  * Pair blocks (bid < Gp NP): tiles (NI-1-p, g) then (p, g).  The first Gx panels in the
+//    XCD-aware order: blocks b and b + 8 share an XCD (dispatch is round-robin over the 8 XCDs),
+//    so the blocks of XCD slot x = b % 8 are laid out in their own order t = b / 8 as groups of
+//    G = kXcdPanels panels (x, x + 8, ...) x all pairs, pair-major: an XCD's 64 resident blocks
+//    hold G panels x 64/G pairs, each K* panel read by 64/G blocks at once and each L^-1 pair by
+//    G (C3 TRMM fabric traffic, FETCH_SIZE x2: plain pair-major 5.09 GB per launch, G = 4 4.52,
+//    G = 8 4.18; launch time unchanged, profiles/r03/ab_map.log).  The rest pair-major.
+//  * Single-tile blocks (bid >= Gp NP): tile (I, g) for the last Qc panels, I descending (the
+//    longest, 8 (I + 1) K steps, first): the dispatcher hands each freed slot the next block, so
+//    the launch's last residency round is packed longest-first instead of leaving CUs idle
+//    behind uniform pairs (trmm_sched).
+GP_DEV void trmm_block_tiles(int bid, const TrmmArgs& a, int& g, int& I0, int& I1) {
+  const int NP = (a.NI + 1) / 2;
+  const int nA = a.Gp * NP;
+  if (bid < nA) {
+    int p;
+    if (bid < a.Gx * NP) {
+      const int x = bid & 7, t = bid >> 3, per = kXcdPanels * NP;
+      const int grp = t / per, j = t - grp * per;
+      p = j / kXcdPanels;
+      g = x + 8 * (grp * kXcdPanels + j % kXcdPanels);
+    } else {
+      const int r = bid - a.Gx * NP, Gr = a.Gp - a.Gx;
+      p = r / Gr;
+      g = a.Gx + (r - p * Gr);
+    }
+    I0 = a.NI - 1 - p;
+    I1 = (I0 == p) ? -1 : p;
   } else {
-    p = bid / NC;
-    C = bid - p * NC;
+    const int t = bid - nA;
+    const int q = t / a.Qc;
+    I0 = a.NI - 1 - q;
+    g = a.Gp + (t - q * a.Qc);
+    I1 = -1;
   }
 }
 
@@ -173,26 +229,28 @@ GP_DEV void trmm_block_tile(int bid, int NI, int NC, int& p, int& C) {
 #endif
 constexpr bool kDiagFirst = TRMM_DIAG_FIRST;
 
-// Row-tile pairs: block (p, C) computes tile (NI-1-p, C) and then tile (p, C), so every block
-// runs 8(NI+1) K steps (uniform work: at C3 the 512 blocks of a chunk are exactly one
-// residency wave of 2 per CU, no tail) and the second tile's first stage is fetched under the
-// first tile's last MFMAs.  Per K step: the next stage's global_load_lds is issued, then the
-// MFMAs of the current stage, then one vmcnt(0) + barrier.
-__global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
-    const double* __restrict__ Linv, int ld, long long sL, const double* __restrict__ Kt2,
-    int mc, long long sK, const double* __restrict__ z, int npad, double* __restrict__ part,
-    int NI, int NC) {
+GP_DEV bool trmm_diag_first(int I, int NI) { return kDiagFirst && 2 * I < NI - 1; }
+
+// Row-tile pairs: block (p, g) computes tile (NI-1-p, g) and then tile (p, g), so every pair
+// block runs 8(NI+1) K steps (uniform work: at C3 the 512 blocks of a residency round finish
+// together) and the second tile's first stage is fetched under the first tile's last MFMAs;
+// single-tile blocks (trmm_block_tiles) fill a launch's last round.  Per K step: the next
+// stage's global_load_lds is issued, then the MFMAs of the current stage, then one vmcnt(0) +
+// barrier.
+__global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
-  const int b = blockIdx.y;
-  int p, C;
-  trmm_block_tile(blockIdx.x, NI, NC, p, C);
-  const int Ihi = NI - 1 - p, Ilo = p;
-  const int npass = (Ihi == Ilo) ? 1 : 2;
+  const int NI = a.NI, mc = a.mc, ld = a.ld;
+  int g, Ifirst, Isecond;
+  trmm_block_tiles(blockIdx.x, a, g, Ifirst, Isecond);
+  const int b = g / a.NCt, Cl = g - b * a.NCt;       // problem, panel of the launch
+  const int chr = Cl / a.NCc, C = Cl - chr * a.NCc;   // chunk (relative), panel in the chunk
+  const int npass = (Isecond < 0) ? 1 : 2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1, li = lane & 15, lk = lane >> 4;
-  const double* Lb = Linv + b * sL + 2 * lane;                          // + I*BI + k*ld
-  const double* K = Kt2 + b * sK + (long long)C * BC + 2 * lane;       // + k*mc per row
+  const double* Lb = a.Linv + b * a.sL + 2 * lane;                      // + I*BI + k*ld
+  const double* K = a.Kt2 + chr * a.slab + b * a.sK + (long long)C * BC + 2 * lane;  // + k*mc
+  double* const part = a.part + chr * a.pslab;
 
   auto issue = [&](const double* L, int s, double* st) {
     const int k0 = s * BK;
@@ -207,24 +265,26 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
       glds16(K + (long long)(k0 + kr) * mc, st + ASTAGE + kr * BC);
     }
   };
+  // a tile's first K step: its diagonal block's when it runs that block first
+  auto first_step = [&](int I) { return trmm_diag_first(I, NI) ? I * (BI / BK) : 0; };
 
-  issue(Lb + Ihi * BI, 0, smem);
+  issue(Lb + Ifirst * BI, first_step(Ifirst), smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll 1
   for (int pass = 0; pass < npass; ++pass) {
-    const int I = pass ? Ilo : Ihi;
+    const int I = pass ? Isecond : Ifirst;
     const double* L = Lb + I * BI;
     const int nsteps = (I + 1) * (BI / BK);   // even: the last step reads stage buffer 1
     f64x4 acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int i4 = 0; i4 < 4; ++i4)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[a][c] = zero4();
+      for (int c = 0; c < 4; ++c) acc[i4][c] = zero4();
     const int s_diag = nsteps - BI / BK;
     int nst = nsteps;
     asm volatile("" : "+s"(nst));
-    if (kDiagFirst && pass == 1) {
+    if (trmm_diag_first(I, NI)) {
       // the second tile: its diagonal block first (k-steps s_diag .., t = s), then k-steps 0 ..
       for (int s = 0; s < BI / BK; ++s) {
         double* cur = smem + (s & 1) * STAGE;
@@ -254,7 +314,7 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
         double* cur = smem + (s & 1) * STAGE;
         if (s + 1 < nst) issue(L, s + 1, smem + ((s + 1) & 1) * STAGE);
         else if (pass + 1 < npass)               // next tile's first stage
-          issue(Lb + Ilo * BI, kDiagFirst ? Ilo * (BI / BK) : 0, smem);
+          issue(Lb + Isecond * BI, first_step(Isecond), smem);
         const int t = s - s_diag;               // the wave's last row tile is 7 - wr
         if (t <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, t);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -264,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
 
     // epilogue in stage buffer 1 (buffer 0 may hold the next tile's first stage)
     double* red = smem + STAGE;
-    const double* zb = z + (long long)b * npad + I * BI;
+    const double* zb = a.z + (long long)b * a.npad + I * BI;
     double zr[4][4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -302,8 +362,9 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(
   }
 }
 
-// mean / var of test points [j0, j0 + mv): column j's partial sums sit in chunk j / mc's slab
-// (slabs pslab doubles apart; pslab = 0 when every chunk reuses one slab).
+// mean / var of test points [j0, j0 + mv): column j's partial sums sit in the slab of chunk
+// j / mc, counted from j0's chunk (slabs pslab doubles apart after `part`; pslab = 0 when every
+// chunk reuses one slab).
 __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ part, int NI,
                                                        int mc, long long pslab, int j0, int mv,
                                                        const double* __restrict__ s_pred,
@@ -312,9 +373,9 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
   const int b = blockIdx.y;
   const int jl = blockIdx.x * 256 + threadIdx.x;
   if (jl >= mv) return;
-  const int j = j0 + jl, ch = j / mc, jj = j - ch * mc;
-  const double* pm = part + ch * pslab + (long long)(b * 2 + 0) * NI * mc + jj;
-  const double* pv = part + ch * pslab + (long long)(b * 2 + 1) * NI * mc + jj;
+  const int j = j0 + jl, ch = j / mc, jj = j - ch * mc, chr = ch - j0 / mc;
+  const double* pm = part + chr * pslab + (long long)(b * 2 + 0) * NI * mc + jj;
+  const double* pv = part + chr * pslab + (long long)(b * 2 + 1) * NI * mc + jj;
   double sm = 0.0, sv = 0.0;
 #pragma unroll 8
   for (int I = 0; I < NI; ++I) {
@@ -353,63 +414,67 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
                                batch, st);
 }
 
-// z = L^-1 w for the prediction in two deterministic passes.  The one-pass trmv_kernel
-// (linalg.hip) has n/64 blocks, 64 at n = 4096, each walking up to n columns with two loads in
-// flight per lane: 90 us alone, 220 us beside the tail of the cross-covariance, and it sits
-// between the factorisation and the first TRMM (profiles/r02/step_timeline_f2d.txt).
-//   pass 1: block (rb, kt) forms row block rb's (64 rows) product with column tile kt (kZT
-//           = 128 columns; tiles on or below the diagonal only: ~1056 blocks at n = 4096),
-//           4 waves x 32 columns, all 32 loads in flight per lane, into zp[kt][r];
-//   pass 2: z[r] = sum over kt = 0 .. last tile of r's row block of zp[kt][r], in tile order.
+// z = L^-1 w for the prediction in two deterministic passes (the same arithmetic whatever the
+// chunking, so results stay bit-identical across m_chunk).  z sits between the factorisation
+// and the first TRMM, on the critical path of every step.  Round 4's form (64-row blocks x
+// 128-column tiles, 32 loads of 512 B per wave at a 32 KB column stride) read the 71 MB
+// triangle in 95 us alone, 140 us beside the cross-covariance (0.06 of HBM,
+// profiles/r04/r04k_timeline.txt).  Here every load instruction of a block reads 4 KB of one
+// column:
+//   pass 1: block (rb, s) forms row block rb's kZR rows (2 per thread, one 16-B load per
+//           column) times column strip s (kZS columns; strips right of the row block are zero
+//           and skipped: 288 blocks at n = 4096), k ascending, into zp[s][r];
+//   pass 2: z[r] = sum over s = 0 .. last strip of r's row block of zp[s][r], in strip order.
 // Every row r < npad is written (rows >= n are 0: L^-1 is zero-padded).  zp (batch *
-// ceil(npad / kZT) * npad doubles, 1 MB per problem at n = 4096) is its own workspace region.
-constexpr int kZT = 128;
-constexpr int kZW = kZT / 4;   // columns per wave
+// ceil(npad / kZS) * npad doubles, 2 MB per problem at n = 4096) is its own workspace region.
+constexpr int kZR = 512;   // rows per pass-1 block
+constexpr int kZS = 64;    // columns per strip
 
 __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict__ Linv, int ld,
                                                         long long sL,
                                                         const double* __restrict__ w, int ldw,
                                                         double* __restrict__ zp, int npad,
                                                         int n) {
-  const int b = blockIdx.z, rb = blockIdx.x * 64, k0 = blockIdx.y * kZT;
-  if (k0 > rb + 63 || k0 >= n) return;            // above the diagonal: pass 2 skips it
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const double* L = Linv + b * sL + rb + lane;
+  const int b = blockIdx.z, rb = blockIdx.x * kZR, k0 = blockIdx.y * kZS;
+  if (k0 > rb + kZR - 1 || k0 >= n) return;       // right of the row block: pass 2 skips it
+  const int r = rb + 2 * threadIdx.x;
+  if (r >= npad) return;                           // npad is even: both rows or neither
+  const double* L = Linv + b * sL + r;
   const double* wb = w + (long long)b * ldw;
-  const int kb = k0 + wv * kZW;
-  const int ke = min(kb + kZW, min(n, rb + 64));  // L^-1 is zero right of the diagonal
-  // all of the wave's kZW column loads issued before the first FMA (one latency round instead
-  // of kZW / 8); the sums run in the same order as with 8 loads in flight, so z is unchanged
-  double lv[kZW], wk[kZW];
+  const int ke = min(k0 + kZS, n);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll 1
+  for (int kb = k0; kb < ke; kb += 16) {
+    // 16 columns' loads in flight before the first FMA
+    double2 lv[16];
+    double wk[16];
 #pragma unroll
-  for (int j = 0; j < kZW; ++j) {
-    const bool ok = kb + j < ke;
-    lv[j] = ok ? L[(long long)(kb + j) * ld] : 0.0;
-    wk[j] = ok ? wb[kb + j] : 0.0;
+    for (int j = 0; j < 16; ++j) {
+      const bool ok = kb + j < ke;
+      lv[j] = ok ? *reinterpret_cast<const double2*>(L + (long long)(kb + j) * ld)
+                 : make_double2(0.0, 0.0);
+      wk[j] = ok ? wb[kb + j] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      a0 = fma(lv[j].x, wk[j], a0);
+      a1 = fma(lv[j].y, wk[j], a1);
+    }
   }
-  double acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.0;
-#pragma unroll
-  for (int j = 0; j < kZW; ++j) acc[j & 7] = fma(lv[j], wk[j], acc[j & 7]);
-  __shared__ double red[4][64];
-  red[wv][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  __syncthreads();
-  if (wv == 0)
-    zp[((long long)b * gridDim.y + blockIdx.y) * npad + rb + lane] =
-        (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  *reinterpret_cast<double2*>(zp + ((long long)b * gridDim.y + blockIdx.y) * npad + r) =
+      make_double2(a0, a1);
 }
 
-__global__ __launch_bounds__(256) void trmv_sum_kernel(const double* __restrict__ zp, int nkt,
+__global__ __launch_bounds__(256) void trmv_sum_kernel(const double* __restrict__ zp, int nst,
                                                        int npad, int n, double* __restrict__ z,
                                                        int ldz) {
   const int b = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
   if (r >= npad) return;
-  const int rb = r & ~63;
-  const int last = min(rb + 63, n - 1) / kZT;     // pass 1's tiles for r's row block
-  const double* q = zp + (long long)b * nkt * npad + r;
+  const int rb = (r / kZR) * kZR;
+  const int last = min(rb + kZR - 1, n - 1) / kZS;  // pass 1's strips for r's row block
+  const double* q = zp + (long long)b * nst * npad + r;
   double acc = 0.0;
-  for (int kt = 0; kt <= last; ++kt) acc += q[(long long)kt * npad];
+  for (int s = 0; s <= last; ++s) acc += q[(long long)s * npad];
   z[(long long)b * ldz + r] = acc;
 }
 
@@ -418,8 +483,9 @@ struct Plan {
   long long off_z, off_zp, off_kt, off_part, off_pot, bytes, slab_elems, part_elems;
 };
 
-// slabs = 1: one cross-covariance chunk and one partial-sum slab at a time (gp_predict, which
-// finalises each chunk after its TRMM); slabs = nchunks: every chunk's cross-covariance and
+// slabs = 1 (2 with a partial last chunk): one cross-covariance chunk and one partial-sum slab
+// at a time (gp_predict, which finalises each chunk after its TRMM); slabs = nchunks: every
+// chunk's cross-covariance and
 // partial sums materialised (gp_predict_cross + gp_predict_solve, gp_fit_predict), so one
 // finalize launch after the last TRMM covers all m points.  `potrf`: plus the factorisation's
 // scratch (gp_fit_predict).
@@ -451,10 +517,12 @@ Plan make_plan(int n, int m, int batch, int m_chunk, bool all_slabs = false,
   p.mc = mc;
   p.NC = mc / BC;
   p.nchunks = gp_ceil_div(m, mc);
-  p.slabs = all_slabs ? p.nchunks : 1;
+  // gp_predict with a partial last chunk: two slabs, so that chunk's TRMM can run merged with
+  // the chunk before it (trmm_merge_last)
+  p.slabs = all_slabs ? p.nchunks : (p.nchunks >= 2 && m % mc != 0) ? 2 : 1;
   p.slab_elems = (long long)batch * mc * p.npad;
   long long z = (long long)batch * p.npad;
-  long long zp = (long long)batch * gp_ceil_div(p.npad, kZT) * p.npad;   // trmv partials
+  long long zp = (long long)batch * gp_ceil_div(p.npad, kZS) * p.npad;   // trmv partials
   long long kt = p.slab_elems * p.slabs;
   p.part_elems = (long long)batch * 2 * p.NI * mc;
   const long long part = p.part_elems * p.slabs;
@@ -535,13 +603,13 @@ WS carve(const Plan& p, void* ws) {
 hipError_t trmv_pred(const Plan& p, const WS& w, const double* Linv, int ldinv,
                      long long strideInv, const double* w_hat, int ldw, int n, int batch,
                      hipStream_t stream) {
-  const int nkt = gp_ceil_div(p.npad, kZT);
-  hipLaunchKernelGGL(trmv_part_kernel, dim3(p.npad / 64, nkt, batch), dim3(256), 0, stream,
-                     Linv, ldinv, strideInv, w_hat, ldw, w.zp, p.npad, n);
+  const int nst = gp_ceil_div(p.npad, kZS);
+  hipLaunchKernelGGL(trmv_part_kernel, dim3(gp_ceil_div(p.npad, kZR), nst, batch), dim3(256), 0,
+                     stream, Linv, ldinv, strideInv, w_hat, ldw, w.zp, p.npad, n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(trmv_sum_kernel, dim3(gp_ceil_div(p.npad, 256), batch), dim3(256), 0,
-                     stream, w.zp, nkt, p.npad, n, w.z, p.npad);
+                     stream, w.zp, nst, p.npad, n, w.z, p.npad);
   return hipGetLastError();
 }
 
@@ -554,23 +622,83 @@ hipError_t cross_chunk(const Plan& p, int ch, double* kt, const double* X, int l
                          p.mc, p.npad, (long long)p.mc * p.npad, batch, stream);
 }
 
-// TRMM of chunk ch into partial-sum slab `part`; with `fin`, also its mean / var.
-hipError_t solve_chunk(const Plan& p, int ch, double* part, const double* z, const double* kt,
-                       const double* Linv, int ldinv, long long strideInv, int m,
-                       const double* s_pred, double* mean, double* var, int ldo, int batch,
-                       bool fin, hipStream_t stream) {
-  const int c0 = ch * p.mc;
-  const int mv = (m - c0 < p.mc) ? (m - c0) : p.mc;
-  const int ncol_tiles = gp_ceil_div(mv, BC);
-  if (fin) gpfit_prof_begin(GP_PROF_TRMM, stream);
-  hipLaunchKernelGGL(trmm_pair_kernel, dim3((p.NI + 1) / 2 * ncol_tiles, batch), dim3(256), 0,
-                     stream, Linv, ldinv, strideInv, kt, p.mc, (long long)p.mc * p.npad, z,
-                     p.npad, part, p.NI, ncol_tiles);
-  if (fin) gpfit_prof_end(GP_PROF_TRMM, stream);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !fin) return e;
-  hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0, stream,
-                     part, p.NI, p.mc, 0LL, c0, mv, s_pred, mean, var, ldo);
+// Residency slots of trmm_pair_kernel on the current device (CUs x blocks per CU), cached.
+int trmm_slots() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  int ncu = 0, nb = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu < 1)
+    ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, trmm_pair_kernel, 256, 0) !=
+          hipSuccess ||
+      nb < 1)
+    nb = 2;
+  v = ncu * nb;
+  cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
+
+// The schedule of one launch over G = batch * NCt panels (T = G * NP pair blocks, S slots).
+// Whole residency rounds of uniform pair blocks finish together; a partial last round would
+// leave CUs idle for a whole pair block's time (C3's 1696-point tail: 224 blocks for 512
+// slots, 0.535 ms against 0.414 at the full rate; a rank's 13,408 points at 8 ranks: 3.28
+// rounds, the last 0.28 taking a full block's time).  So when T is not a multiple of S, the
+// panels of the last round and one full round before it run as single-tile blocks, longest
+// first: S blocks start on the longest tiles and every slot that frees takes the next, so the
+// launch ends within about one short tile of T / S pair-block times.
+void trmm_sched(TrmmArgs& a, int batch, int slots) {
+  const int NP = (a.NI + 1) / 2;
+  const long long G = (long long)batch * a.NCt;
+  const long long T = G * NP;
+  long long Gp = G;
+  if (slots > 0 && T % slots != 0) {
+    const long long full = T / slots;
+    Gp = (full > 0 ? full - 1 : 0) * slots / NP;
+  }
+  a.Gp = (int)Gp;
+  a.Qc = (int)(G - Gp);
+  const int grp = 8 * kXcdPanels;
+  a.Gx = grp > 0 ? (a.Gp / grp) * grp : 0;
+}
+
+// The last chunk's TRMM runs merged with the one before it when its blocks fill less than one
+// residency round (the merged launch's schedule then packs that round with the previous
+// chunk's panels).
+bool trmm_merge_last(const Plan& p, int m, int batch) {
+  if (p.nchunks < 2 || m % p.mc == 0) return false;
+  const long long tail_panels = gp_ceil_div(m - (p.nchunks - 1) * p.mc, BC);
+  return (long long)batch * tail_panels * ((p.NI + 1) / 2) < trmm_slots();
+}
+
+// TRMM of chunks ch0 .. ch1 (consecutive; each chunk's cross-covariance `slab` doubles after the
+// one before, its partial sums `pslab` after) in one launch.
+hipError_t trmm_launch(const Plan& p, int ch0, int ch1, const double* kt, long long slab,
+                       double* part, long long pslab, const double* z, const double* Linv,
+                       int ldinv, long long strideInv, int m, int batch, hipStream_t stream) {
+  const int c1 = ch1 * p.mc;
+  const int mv1 = (m - c1 < p.mc) ? (m - c1) : p.mc;
+  TrmmArgs a;
+  a.Linv = Linv;
+  a.sL = strideInv;
+  a.Kt2 = kt;
+  a.sK = (long long)p.mc * p.npad;
+  a.slab = slab;
+  a.z = z;
+  a.part = part;
+  a.pslab = pslab;
+  a.ld = ldinv;
+  a.mc = p.mc;
+  a.NCc = p.NC;
+  a.NCt = (ch1 - ch0) * p.NC + gp_ceil_div(mv1, BC);
+  a.npad = p.npad;
+  a.NI = p.NI;
+  trmm_sched(a, batch, trmm_slots());
+  const long long blocks = (long long)a.Gp * ((p.NI + 1) / 2) + (long long)a.Qc * p.NI;
+  hipLaunchKernelGGL(trmm_pair_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -586,25 +714,31 @@ hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
                      const hipEvent_t* ready, int late, Cross&& cross) {
   hipError_t e;
   if (ready && late > 0 && (e = hipStreamWaitEvent(stream, ready[0], 0)) != hipSuccess) return e;
+  const bool merge = trmm_merge_last(p, m, batch);
+  const int nlaunch = p.nchunks - (merge ? 1 : 0);
   // timing: one event pair spans the back-to-back TRMM launches (an event record between
   // launches costs a few us of stream time each); gp_profile_read reports it per launch.
   // With late cross-covariance chunks in between, one pair per launch.
   const bool split = late < p.nchunks;
-  if (!split) gpfit_prof_begin_n(GP_PROF_TRMM, stream, p.nchunks);
-  for (int ch = 0; ch < p.nchunks; ++ch) {
-    if (ch >= late) {
-      gpfit_prof_begin(GP_PROF_CROSS, stream);
-      if ((e = cross(ch)) != hipSuccess) return e;
-      gpfit_prof_end(GP_PROF_CROSS, stream);
-    } else if (ready && ch > 0 && (e = hipStreamWaitEvent(stream, ready[ch], 0)) != hipSuccess) {
-      return e;
+  if (!split) gpfit_prof_begin_n(GP_PROF_TRMM, stream, nlaunch);
+  for (int ch = 0; ch < p.nchunks;) {
+    const int ch1 = (merge && ch == p.nchunks - 2) ? ch + 1 : ch;
+    for (int c = ch; c <= ch1; ++c) {
+      if (c >= late) {
+        gpfit_prof_begin(GP_PROF_CROSS, stream);
+        if ((e = cross(c)) != hipSuccess) return e;
+        gpfit_prof_end(GP_PROF_CROSS, stream);
+      } else if (ready && c > 0 && (e = hipStreamWaitEvent(stream, ready[c], 0)) != hipSuccess) {
+        return e;
+      }
     }
     if (split) gpfit_prof_begin(GP_PROF_TRMM, stream);
-    e = solve_chunk(p, ch, w.part + ch * p.part_elems, w.z,
-                               w.kt + (long long)ch * p.slab_elems, Linv, ldinv, strideInv, m,
-                               s_pred, mean, var, ldo, batch, false, stream);
+    e = trmm_launch(p, ch, ch1, w.kt + (long long)ch * p.slab_elems, p.slab_elems,
+                    w.part + ch * p.part_elems, p.part_elems, w.z, Linv, ldinv, strideInv, m,
+                    batch, stream);
     if (e != hipSuccess) return e;
     if (split) gpfit_prof_end(GP_PROF_TRMM, stream);
+    ch = ch1 + 1;
   }
   if (!split) gpfit_prof_end(GP_PROF_TRMM, stream);
   hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(m, 256), batch), dim3(256), 0, stream,
@@ -633,12 +767,28 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, stream));
+  // chunk by chunk: cross-covariance, TRMM, mean / var, reusing one slab -- except that a
+  // merged last chunk (trmm_merge_last) has its own second slab, and its TRMM and finalize
+  // cover the chunk before it too
+  const bool merge = trmm_merge_last(p, m, batch);
   for (int ch = 0; ch < p.nchunks; ++ch) {
+    const bool held = merge && ch == p.nchunks - 2;   // TRMM deferred to the merged launch
+    const int sl = (merge && ch == p.nchunks - 1) ? 1 : 0;
     gpfit_prof_begin(GP_PROF_CROSS, stream);
-    GP_CK(cross_chunk(p, ch, w.kt, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch, stream));
+    GP_CK(cross_chunk(p, ch, w.kt + sl * p.slab_elems, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta,
+                      s, batch, stream));
     gpfit_prof_end(GP_PROF_CROSS, stream);
-    GP_CK(solve_chunk(p, ch, w.part, w.z, w.kt, Linv, ldinv, strideInv, m, s_pred, mean, var,
-                      ldo, batch, true, stream));
+    if (held) continue;
+    const int ch0 = (merge && ch == p.nchunks - 1) ? ch - 1 : ch;
+    gpfit_prof_begin(GP_PROF_TRMM, stream);
+    GP_CK(trmm_launch(p, ch0, ch, w.kt, p.slab_elems, w.part, p.part_elems, w.z, Linv, ldinv,
+                      strideInv, m, batch, stream));
+    gpfit_prof_end(GP_PROF_TRMM, stream);
+    const int j0 = ch0 * p.mc;
+    const int mv = (m - j0 < (ch - ch0 + 1) * p.mc) ? m - j0 : (ch - ch0 + 1) * p.mc;
+    hipLaunchKernelGGL(finalize_kernel, dim3(gp_ceil_div(mv, 256), batch), dim3(256), 0, stream,
+                       w.part, p.NI, p.mc, p.part_elems, j0, mv, s_pred, mean, var, ldo);
+    GP_CK(hipGetLastError());
   }
 #undef GP_CK
   return 0;

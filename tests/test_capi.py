@@ -323,3 +323,14 @@ def test_legacy_normal_reproduces_the_reference_omega():
         np.random.seed(123)
         got = legacy_normal_f32(ref.shape, threads=4)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), tag
+
+
+def test_predict_workspace_holds_the_merged_tail(lib):
+    """gp_predict sizes two cross-covariance slabs exactly when the last chunk is partial (so it
+    can run merged with the chunk before it), one otherwise."""
+    full = lib.gp_predict_ws_bytes(1000, 32768, 1, 0)
+    part = lib.gp_predict_ws_bytes(1000, 32768 + 128, 1, 0)
+    one = lib.gp_predict_ws_bytes(1000, 16384, 1, 0)
+    slab = 8 * 1024 * 16384                         # npad x chunk doubles
+    assert part - full >= slab                      # the second slab (+ partial sums)
+    assert full == one                              # whole chunks reuse one slab

@@ -26,7 +26,8 @@ end = max(int(r["End_Timestamp"]) for r in seq)
 print(f"step span {(end - t0) / 1e3:.1f} us")
 for n in sorted(tot, key=lambda k: -tot[k]):
     print(f"  {n:28s} {cnt[n]:5d} launches {tot[n]:9.1f} us")
-tr = [r for r in seq if name(r) in ("trmm_pair_kernel", "finalize_kernel", "trmv_kernel")]
+tr = [r for r in seq if name(r) in ("trmm_pair_kernel", "finalize_kernel", "trmv_kernel",
+                                    "trmv_part_kernel", "trmv_sum_kernel")]
 first_trmv = min(int(r["Start_Timestamp"]) for r in tr)
 last_fact = max(int(r["End_Timestamp"]) for r in seq if name(r).startswith(("chol_", "pp_")))
 last_cross = max(int(r["End_Timestamp"]) for r in seq if name(r).startswith("cross_"))
