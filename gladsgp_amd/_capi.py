@@ -52,6 +52,16 @@ SIGNATURES = {
     "gp_predict": (c_int, [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_int, c_int,
                            c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int, c_void_p]),
+    "gp_predict_ex": (c_int, [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_int, c_int,
+                              c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                              c_void_p, c_void_p, c_int, c_int, c_void_p, c_ll, c_int, c_int,
+                              c_void_p, c_ll, c_void_p]),
+    "gp_predict_z_ws_bytes": (c_ll, [c_int, c_int]),
+    "gp_predict_z": (c_int, [c_void_p, c_int, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_ll,
+                             c_int, c_void_p, c_ll, c_void_p]),
+    "gp_linv_packed_elems": (c_ll, [c_int]),
+    "gp_pack_linv": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "gp_unpack_linv": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "gp_predict_prepared_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
     "gp_predict_cross": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                  c_int, c_void_p, c_int, c_void_p, c_ll, c_int, c_void_p]),
@@ -115,6 +125,7 @@ SIGNATURES = {
 }
 
 PROF_GRAM, PROF_POTRF, PROF_TRMM, PROF_CROSS = 0, 1, 2, 3
+LINV_PADDED, LINV_PACKED = 0, 1        # GPFIT_LINV_PADDED / GPFIT_LINV_PACKED
 
 
 class GPFitUnavailable(RuntimeError):

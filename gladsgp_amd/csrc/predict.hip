@@ -151,6 +151,22 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
 #endif
 constexpr int kXcdPanels = TRMM_XCD_PANELS;
 
+// The tile-packed L^-1 (GPFIT_LINV_PACKED, the single-GP broadcast's payload): column k of the
+// padded npad x npad L^-1 from row 16 floor(k / 16) on, columns one after another, so every
+// stored run starts on a 16-row MFMA tile and is a multiple of 16 doubles (128-B aligned).
+// Element (r, k), r >= 16 floor(k / 16), sits at linv_col(k, npad) + r.  Rows below the start
+// hold other columns' data: the TRMM's diagonal-block steps never use them (row tile r < t is
+// skipped at step t) and the trmv masks them, so results equal the padded layout's bit for bit.
+//   linv_col(k) = k npad - 16 sum_{j < k} floor(j / 16) - 16 floor(k / 16)
+__host__ __device__ inline long long linv_col(long long k, long long npad) {
+  const long long q = k >> 4;
+  return k * npad - 128 * q * (q - 1) - 16 * q * (k - 16 * q) - 16 * q;
+}
+__host__ __device__ inline long long linv_packed_elems(long long npad) {
+  const long long q = npad >> 4;
+  return npad * npad - 128 * q * (q - 1);
+}
+
 // One TRMM launch covers `NCt` column panels of each of `batch` problems -- the panels of one
 // test-point chunk, or of the last two chunks merged (a chunk whose blocks fill less than one
 // residency round runs with the chunk before it, trmm_launch) -- numbered g = b * NCt + C
@@ -163,11 +179,12 @@ constexpr int kXcdPanels = TRMM_XCD_PANELS;
 // that is the second of its row-tile pair, its diagonal block first: trmm_diag_first), so
 // results are bit-identical whatever the chunking and the schedule.
 struct TrmmArgs {
-  const double* Linv;
+  const double* Linv;      // padded (column k at k * ld) or tile-packed (linv_col, PACKED)
   long long sL;
   const double* Kt2;       // the launch's first chunk's cross-covariance slab
   long long sK, slab;      // problem stride inside a slab; slab stride (chunk to chunk)
   const double* z;
+  long long zld;           // z problem stride
   double* part;            // the launch's first chunk's partial-sum slab
   long long pslab;         // partial-sum slab stride
   int ld, mc, NCc, NCt, npad, NI;
@@ -237,6 +254,7 @@ GP_DEV bool trmm_diag_first(int I, int NI) { return kDiagFirst && 2 * I < NI - 1
 // single-tile blocks (trmm_block_tiles) fill a launch's last round.  Per K step: the next
 // stage's global_load_lds is issued, then the MFMAs of the current stage, then one vmcnt(0) +
 // barrier.
+template <bool PACKED>
 __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const int NI = a.NI, mc = a.mc, ld = a.ld;
@@ -257,7 +275,8 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {              // A rows k0 + 4w + r
       const int kr = 4 * w + r;
-      glds16(L + (long long)(k0 + kr) * ld, st + kr * APITCH);
+      const long long col = PACKED ? linv_col(k0 + kr, a.npad) : (long long)(k0 + kr) * ld;
+      glds16(L + col, st + kr * APITCH);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {              // B rows k0 + 4w + r
@@ -324,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
 
     // epilogue in stage buffer 1 (buffer 0 may hold the next tile's first stage)
     double* red = smem + STAGE;
-    const double* zb = a.z + (long long)b * a.npad + I * BI;
+    const double* zb = a.z + b * a.zld + I * BI;
     double zr[4][4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -430,6 +449,7 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
 constexpr int kZR = 512;   // rows per pass-1 block
 constexpr int kZS = 64;    // columns per strip
 
+template <bool PACKED>
 __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict__ Linv, int ld,
                                                         long long sL,
                                                         const double* __restrict__ w, int ldw,
@@ -450,10 +470,14 @@ __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict
     double wk[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const bool ok = kb + j < ke;
-      lv[j] = ok ? *reinterpret_cast<const double2*>(L + (long long)(kb + j) * ld)
+      const int k = kb + j;
+      // tile-packed: rows below column k's first stored tile are zero in L^-1 (the padded
+      // layout's fma(0, w, acc) leaves acc unchanged, so skipping them changes no bit)
+      const bool ok = k < ke && (!PACKED || r >= ((k >> 4) << 4));
+      lv[j] = ok ? *reinterpret_cast<const double2*>(
+                       L + (PACKED ? linv_col(k, npad) : (long long)k * ld))
                  : make_double2(0.0, 0.0);
-      wk[j] = ok ? wb[kb + j] : 0.0;
+      wk[j] = k < ke ? wb[k] : 0.0;
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -467,7 +491,7 @@ __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict
 
 __global__ __launch_bounds__(256) void trmv_sum_kernel(const double* __restrict__ zp, int nst,
                                                        int npad, int n, double* __restrict__ z,
-                                                       int ldz) {
+                                                       long long ldz) {
   const int b = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
   if (r >= npad) return;
   const int rb = (r / kZR) * kZR;
@@ -572,11 +596,12 @@ int check_common(const double* X, int ldx, const double* Xs, int ldxs, int n, in
 
 int check_solve(const double* Linv, int ldinv, long long strideInv, int n, const double* s_pred,
                 const double* w_hat, int ldw, int m, double* mean, double* var, int ldo,
-                int batch) {
+                int batch, bool packed = false) {
   if (!Linv || (reinterpret_cast<uintptr_t>(Linv) & 15)) return -1;
   const int npad = gp_padded_n(n);
-  if (ldinv < npad || ldinv < 1 || (ldinv & 1)) return -2;   // 16-B aligned double2 loads
-  if ((batch > 1 && strideInv < (long long)ldinv * npad) || (strideInv & 1)) return -3;
+  if (!packed && (ldinv < npad || ldinv < 1 || (ldinv & 1))) return -2;   // 16-B double2 loads
+  const long long per = packed ? linv_packed_elems(npad) : (long long)ldinv * npad;
+  if ((batch > 1 && strideInv < per) || (strideInv & 1)) return -3;
   if (!s_pred) return -14;
   if (!w_hat) return -15;
   if (ldw < n && batch > 1) return -16;
@@ -598,18 +623,31 @@ WS carve(const Plan& p, void* ws) {
           base + p.off_pot};
 }
 
-// z = L^-1 w into w.z (npad rows per problem), two passes through w.zp (the same arithmetic
-// whatever the chunking, so results stay bit-identical across m_chunk).
-hipError_t trmv_pred(const Plan& p, const WS& w, const double* Linv, int ldinv,
-                     long long strideInv, const double* w_hat, int ldw, int n, int batch,
-                     hipStream_t stream) {
-  const int nst = gp_ceil_div(p.npad, kZS);
-  hipLaunchKernelGGL(trmv_part_kernel, dim3(gp_ceil_div(p.npad, kZR), nst, batch), dim3(256), 0,
-                     stream, Linv, ldinv, strideInv, w_hat, ldw, w.zp, p.npad, n);
+// L^-1 as the prediction reads it: the padded buffer (column k at k * ld) or the tile-packed
+// vector (linv_col); `stride` doubles from one problem to the next.
+struct LinvRef {
+  const double* p;
+  int ld;
+  long long stride;
+  bool packed;
+};
+
+// z = L^-1 w into z (npad rows per problem, problem stride zld), two passes through zp (the same
+// arithmetic whatever the chunking and the layout, so results stay bit-identical).
+hipError_t trmv_pred(int npad, double* zp, const LinvRef& L, const double* w_hat, int ldw,
+                     int n, int batch, double* z, long long zld, hipStream_t stream) {
+  const int nst = gp_ceil_div(npad, kZS);
+  const dim3 grid(gp_ceil_div(npad, kZR), nst, batch);
+  if (L.packed)
+    hipLaunchKernelGGL(trmv_part_kernel<true>, grid, dim3(256), 0, stream, L.p, L.ld, L.stride,
+                       w_hat, ldw, zp, npad, n);
+  else
+    hipLaunchKernelGGL(trmv_part_kernel<false>, grid, dim3(256), 0, stream, L.p, L.ld, L.stride,
+                       w_hat, ldw, zp, npad, n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(trmv_sum_kernel, dim3(gp_ceil_div(p.npad, 256), batch), dim3(256), 0,
-                     stream, w.zp, nst, p.npad, n, w.z, p.npad);
+  hipLaunchKernelGGL(trmv_sum_kernel, dim3(gp_ceil_div(npad, 256), batch), dim3(256), 0,
+                     stream, zp, nst, npad, n, z, zld);
   return hipGetLastError();
 }
 
@@ -633,7 +671,7 @@ int trmm_slots() {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu < 1)
     ncu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, trmm_pair_kernel, 256, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, trmm_pair_kernel<false>, 256, 0) !=
           hipSuccess ||
       nb < 1)
     nb = 2;
@@ -677,20 +715,21 @@ bool trmm_merge_last(const Plan& p, int m, int batch) {
 // TRMM of chunks ch0 .. ch1 (consecutive; each chunk's cross-covariance `slab` doubles after the
 // one before, its partial sums `pslab` after) in one launch.
 hipError_t trmm_launch(const Plan& p, int ch0, int ch1, const double* kt, long long slab,
-                       double* part, long long pslab, const double* z, const double* Linv,
-                       int ldinv, long long strideInv, int m, int batch, hipStream_t stream) {
+                       double* part, long long pslab, const double* z, long long zld,
+                       const LinvRef& L, int m, int batch, hipStream_t stream) {
   const int c1 = ch1 * p.mc;
   const int mv1 = (m - c1 < p.mc) ? (m - c1) : p.mc;
   TrmmArgs a;
-  a.Linv = Linv;
-  a.sL = strideInv;
+  a.Linv = L.p;
+  a.sL = L.stride;
   a.Kt2 = kt;
   a.sK = (long long)p.mc * p.npad;
   a.slab = slab;
   a.z = z;
+  a.zld = zld;
   a.part = part;
   a.pslab = pslab;
-  a.ld = ldinv;
+  a.ld = L.ld;
   a.mc = p.mc;
   a.NCc = p.NC;
   a.NCt = (ch1 - ch0) * p.NC + gp_ceil_div(mv1, BC);
@@ -698,7 +737,10 @@ hipError_t trmm_launch(const Plan& p, int ch0, int ch1, const double* kt, long l
   a.NI = p.NI;
   trmm_sched(a, batch, trmm_slots());
   const long long blocks = (long long)a.Gp * ((p.NI + 1) / 2) + (long long)a.Qc * p.NI;
-  hipLaunchKernelGGL(trmm_pair_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  if (L.packed)
+    hipLaunchKernelGGL(trmm_pair_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(trmm_pair_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -708,10 +750,10 @@ hipError_t trmm_launch(const Plan& p, int ch0, int ch1, const double* kt, long l
 // Chunks from `late` on (gp_fit_predict with gp_ctx_set_aux_chunks) have no cross-covariance
 // yet: `cross(ch)` enqueues it on `stream` just before that chunk's TRMM.
 template <typename Cross>
-hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
-                     long long strideInv, int m, const double* s_pred, double* mean,
-                     double* var, int ldo, int batch, hipStream_t stream,
-                     const hipEvent_t* ready, int late, Cross&& cross) {
+hipError_t solve_all(const Plan& p, const WS& w, const LinvRef& L, const double* z,
+                     long long zld, int m, const double* s_pred, double* mean, double* var,
+                     int ldo, int batch, hipStream_t stream, const hipEvent_t* ready, int late,
+                     Cross&& cross) {
   hipError_t e;
   if (ready && late > 0 && (e = hipStreamWaitEvent(stream, ready[0], 0)) != hipSuccess) return e;
   const bool merge = trmm_merge_last(p, m, batch);
@@ -734,8 +776,7 @@ hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
     }
     if (split) gpfit_prof_begin(GP_PROF_TRMM, stream);
     e = trmm_launch(p, ch, ch1, w.kt + (long long)ch * p.slab_elems, p.slab_elems,
-                    w.part + ch * p.part_elems, p.part_elems, w.z, Linv, ldinv, strideInv, m,
-                    batch, stream);
+                    w.part + ch * p.part_elems, p.part_elems, z, zld, L, m, batch, stream);
     if (e != hipSuccess) return e;
     if (split) gpfit_prof_end(GP_PROF_TRMM, stream);
     ch = ch1 + 1;
@@ -748,25 +789,34 @@ hipError_t solve_all(const Plan& p, const WS& w, const double* Linv, int ldinv,
 
 }  // namespace
 
-extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, const double* X,
-                          int ldx, const double* Xs, int ldxs, int n, int m, int d,
-                          const double* beta, int ldbeta, const double* s,
-                          const double* s_pred, const double* w_hat, int ldw, double* mean,
-                          double* var, int ldo, int batch, void* ws, long long ws_bytes,
-                          int m_chunk, hipStream_t stream) {
+extern "C" int gp_predict_ex(const double* Linv, int ldinv, long long strideInv,
+                             const double* X, int ldx, const double* Xs, int ldxs, int n, int m,
+                             int d, const double* beta, int ldbeta, const double* s,
+                             const double* s_pred, const double* w_hat, int ldw, double* mean,
+                             double* var, int ldo, int batch, void* ws, long long ws_bytes,
+                             int m_chunk, int layout, const double* z, long long ldz,
+                             hipStream_t stream) {
+  if (layout != GPFIT_LINV_PADDED && layout != GPFIT_LINV_PACKED) return -24;
+  const bool packed = layout == GPFIT_LINV_PACKED;
   int rc = check_common(X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch);
   if (rc) return rc;
-  rc = check_solve(Linv, ldinv, strideInv, n, s_pred, w_hat, ldw, m, mean, var, ldo, batch);
+  // with z given, w_hat is not read
+  rc = check_solve(Linv, ldinv, strideInv, n, s_pred, z ? s_pred : w_hat, ldw, m, mean, var, ldo,
+                   batch, packed);
   if (rc) return rc;
+  if (z && (batch > 1 && ldz < gp_padded_n(n))) return -26;
   if (n == 0 || m == 0 || batch == 0) return 0;
   if (m_chunk < 0) return -23;
   const Plan p = make_plan(n, m, batch, m_chunk);
   if (!ws) return -21;
   if (ws_bytes < p.bytes) return -22;
   const WS w = carve(p, ws);
+  const LinvRef L{Linv, ldinv, strideInv, packed};
+  const double* zz = z ? z : w.z;
+  const long long zld = z ? ldz : p.npad;
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
-  GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, stream));
+  if (!z) GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, stream));
   // chunk by chunk: cross-covariance, TRMM, mean / var, reusing one slab -- except that a
   // merged last chunk (trmm_merge_last) has its own second slab, and its TRMM and finalize
   // cover the chunk before it too
@@ -781,8 +831,8 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
     if (held) continue;
     const int ch0 = (merge && ch == p.nchunks - 1) ? ch - 1 : ch;
     gpfit_prof_begin(GP_PROF_TRMM, stream);
-    GP_CK(trmm_launch(p, ch0, ch, w.kt, p.slab_elems, w.part, p.part_elems, w.z, Linv, ldinv,
-                      strideInv, m, batch, stream));
+    GP_CK(trmm_launch(p, ch0, ch, w.kt, p.slab_elems, w.part, p.part_elems, zz, zld, L, m, batch,
+                      stream));
     gpfit_prof_end(GP_PROF_TRMM, stream);
     const int j0 = ch0 * p.mc;
     const int mv = (m - j0 < (ch - ch0 + 1) * p.mc) ? m - j0 : (ch - ch0 + 1) * p.mc;
@@ -792,6 +842,103 @@ extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, co
   }
 #undef GP_CK
   return 0;
+}
+
+extern "C" int gp_predict(const double* Linv, int ldinv, long long strideInv, const double* X,
+                          int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                          const double* beta, int ldbeta, const double* s,
+                          const double* s_pred, const double* w_hat, int ldw, double* mean,
+                          double* var, int ldo, int batch, void* ws, long long ws_bytes,
+                          int m_chunk, hipStream_t stream) {
+  return gp_predict_ex(Linv, ldinv, strideInv, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s,
+                       s_pred, w_hat, ldw, mean, var, ldo, batch, ws, ws_bytes, m_chunk,
+                       GPFIT_LINV_PADDED, nullptr, 0, stream);
+}
+
+// z = L^-1 w alone, with the prediction's arithmetic (the z gp_predict forms internally, bit
+// for bit): rank 0 of the sharded single-GP path ships it with L^-1.  Scratch: the trmv
+// partials.
+extern "C" long long gp_predict_z_ws_bytes(int n, int batch) {
+  if (n <= 0 || batch <= 0) return 0;
+  const long long npad = gp_padded_n(n);
+  return ((8LL * batch * gp_ceil_div(npad, kZS) * npad + 255) / 256) * 256;
+}
+
+extern "C" int gp_predict_z(const double* Linv, int ldinv, long long strideInv, int layout,
+                            int n, const double* w_hat, int ldw, double* z, long long ldz,
+                            int batch, void* ws, long long ws_bytes, hipStream_t stream) {
+  if (!Linv || (reinterpret_cast<uintptr_t>(Linv) & 15)) return -1;
+  if (layout != GPFIT_LINV_PADDED && layout != GPFIT_LINV_PACKED) return -4;
+  const bool packed = layout == GPFIT_LINV_PACKED;
+  if (n < 0) return -5;
+  const int npad = gp_padded_n(n);
+  if (!packed && (ldinv < npad || (ldinv & 1))) return -2;
+  const long long per = packed ? linv_packed_elems(npad) : (long long)ldinv * npad;
+  if ((batch > 1 && strideInv < per) || (strideInv & 1)) return -3;
+  if (!w_hat) return -6;
+  if (ldw < n && batch > 1) return -7;
+  if (!z) return -8;
+  if (ldz < npad && batch > 1) return -9;
+  if (batch < 0) return -10;
+  if (n == 0 || batch == 0) return 0;
+  if (!ws) return -11;
+  if (ws_bytes < gp_predict_z_ws_bytes(n, batch)) return -12;
+  const hipError_t e = trmv_pred(npad, static_cast<double*>(ws), LinvRef{Linv, ldinv, strideInv,
+                                 packed}, w_hat, ldw, n, batch, z, ldz, stream);
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+// The tile-packed layout (linv_col): gp_linv_packed_elems doubles per problem; pack from and
+// unpack into the padded buffer (unpack writes every stored element: the rows below a column's
+// first tile are left as they are, zero in a buffer prepared for gp_predict).
+extern "C" long long gp_linv_packed_elems(int n) {
+  if (n <= 0) return 0;
+  return linv_packed_elems(gp_padded_n(n));
+}
+
+namespace {
+__global__ __launch_bounds__(256) void linv_pack_kernel(const double* __restrict__ A, int npad,
+                                                        long long ld, double* __restrict__ P,
+                                                        int unpack) {
+  const int c = blockIdx.x;
+  const int r0 = (c >> 4) << 4;
+  double* col = const_cast<double*>(A) + (long long)c * ld;
+  double* pc = P + linv_col(c, npad);
+  // 16-B vectors: r0, ld, npad and linv_col are even
+  for (int r = r0 + 2 * threadIdx.x; r < npad; r += 512) {
+    if (!unpack)
+      *reinterpret_cast<double2*>(pc + r) = *reinterpret_cast<const double2*>(col + r);
+    else
+      *reinterpret_cast<double2*>(col + r) = *reinterpret_cast<const double2*>(pc + r);
+  }
+}
+}  // namespace
+
+extern "C" int gp_pack_linv(const double* Linv, int n, int ldinv, double* P, hipStream_t stream) {
+  if (!Linv || (reinterpret_cast<uintptr_t>(Linv) & 15)) return -1;
+  if (n < 0) return -2;
+  const int npad = gp_padded_n(n);
+  if (ldinv < npad || (ldinv & 1)) return -3;
+  if (!P || (reinterpret_cast<uintptr_t>(P) & 15)) return -4;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(linv_pack_kernel, dim3(npad), dim3(256), 0, stream, Linv, npad,
+                     (long long)ldinv, P, 0);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+extern "C" int gp_unpack_linv(const double* P, int n, double* Linv, int ldinv,
+                              hipStream_t stream) {
+  if (!P || (reinterpret_cast<uintptr_t>(P) & 15)) return -1;
+  if (n < 0) return -2;
+  const int npad = gp_padded_n(n);
+  if (!Linv || (reinterpret_cast<uintptr_t>(Linv) & 15)) return -3;
+  if (ldinv < npad || (ldinv & 1)) return -4;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(linv_pack_kernel, dim3(npad), dim3(256), 0, stream, Linv, npad,
+                     (long long)ldinv, const_cast<double*>(P), 1);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }
 
 extern "C" int gp_predict_cross(const double* X, int ldx, const double* Xs, int ldxs, int n,
@@ -834,9 +981,10 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
   const WS w = carve(p, ws);
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
-  GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, stream));
-  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, stream,
-                  nullptr, p.nchunks, [](int) { return hipSuccess; }));
+  const LinvRef L{Linv, ldinv, strideInv, false};
+  GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, stream));
+  GP_CK(solve_all(p, w, L, w.z, p.npad, m, s_pred, mean, var, ldo, batch, stream, nullptr,
+                  p.nchunks, [](int) { return hipSuccess; }));
 #undef GP_CK
   return 0;
 }
@@ -1031,8 +1179,9 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
     if (n_aux > 0) GP_CK(hipEventRecord(S->e_chunk[n_aux - 1], aux));   // after the end event
     GP_CK(hipStreamWaitEvent(pred, S->e_fact, 0));
   }
-  GP_CK(trmv_pred(p, w, Linv, ldinv, strideInv, w_hat, ldw, n, batch, pred));
-  GP_CK(solve_all(p, w, Linv, ldinv, strideInv, m, s_pred, mean, var, ldo, batch, pred,
+  const LinvRef L{Linv, ldinv, strideInv, false};
+  GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, pred));
+  GP_CK(solve_all(p, w, L, w.z, p.npad, m, s_pred, mean, var, ldo, batch, pred,
                   S ? S->e_chunk.data() : nullptr, n_aux, [&](int ch) {
                     return cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs,
                                        ldxs, n, m, d, beta, ldbeta, s, batch, pred);

@@ -188,27 +188,96 @@ PredictWorkspace = Workspace   # scratch of predict / fit_predict / predict_prep
 _DEFAULT_WS = PredictWorkspace()
 
 
-def predict(chol: Cholesky, X: torch.Tensor, Xs: torch.Tensor, beta, s, s_pred, w,
+@dataclass
+class PackedLinv:
+    """L^-1 in the tile-packed layout (gp_pack_linv: column c of the padded buffer from row
+    16 floor(c/16) on, about half the padded square) -- the single-GP broadcast's payload, which
+    :func:`predict` reads in place -- with, optionally, z = L^-1 w (gp_predict_z)."""
+
+    n: int
+    buf: torch.Tensor                 # (batch, gp_linv_packed_elems(n)) float64
+    info: torch.Tensor                # (batch,) int32
+    z: torch.Tensor | None = None     # (batch, padded_n(n)) float64
+
+    def check(self) -> None:
+        check_info(self.info)
+
+
+def linv_packed_elems(n: int) -> int:
+    return int(_capi.lib().gp_linv_packed_elems(int(n)))
+
+
+def pack_linv(chol: Cholesky, out: torch.Tensor | None = None) -> torch.Tensor:
+    """The tile-packed L^-1 of every problem: (batch, gp_linv_packed_elems(n)) (gp_pack_linv)."""
+    batch, npad = chol.linv_buf.shape[0], chol.linv_buf.shape[1]
+    E = linv_packed_elems(chol.n)
+    if out is None:
+        out = torch.empty((batch, E), dtype=F64, device=chol.linv_buf.device)
+    for b in range(batch):
+        _capi.call("gp_pack_linv", chol.linv_buf[b].data_ptr(), chol.n, npad,
+                   out[b].data_ptr(), _stream(out.device))
+    return out
+
+
+_Z_WS = {}
+
+
+def predict_z(chol, w, out: torch.Tensor | None = None) -> torch.Tensor:
+    """z = L^-1 w per problem, (batch, padded_n(n)), zero past n, with exactly the arithmetic
+    :func:`predict` applies internally (gp_predict_z); ``chol`` a Cholesky or a PackedLinv."""
+    packed = isinstance(chol, PackedLinv)
+    L = chol.buf if packed else chol.linv_buf
+    dev, batch, n = L.device, L.shape[0], chol.n
+    npad = padded_n(n)
+    w_t = _as_f64(w, dev, "w").reshape(batch, n)
+    if out is None:
+        out = torch.empty((batch, npad), dtype=F64, device=dev)
+    nbytes = int(_capi.lib().gp_predict_z_ws_bytes(n, batch))
+    ws = _Z_WS.setdefault(str(dev), Workspace()).get(nbytes, dev)
+    _capi.call("gp_predict_z", L.data_ptr(), npad, L.stride(0),
+               _capi.LINV_PACKED if packed else _capi.LINV_PADDED, n, w_t.data_ptr(), n,
+               out.data_ptr(), out.stride(0) if batch > 1 else npad, batch, ws.data_ptr(),
+               ws.numel(), _stream(dev))
+    return out
+
+
+def predict(chol, X: torch.Tensor, Xs: torch.Tensor, beta, s, s_pred, w,
             m_chunk: int = 0, workspace: PredictWorkspace | None = None,
-            out: tuple[torch.Tensor, torch.Tensor] | None = None):
-    """Posterior mean / marginal variance at Xs for every problem: returns (batch, m) x 2."""
-    dev = chol.linv_buf.device
+            out: tuple[torch.Tensor, torch.Tensor] | None = None,
+            z: torch.Tensor | None = None):
+    """Posterior mean / marginal variance at Xs for every problem: returns (batch, m) x 2.
+
+    ``chol`` is a :class:`Cholesky` (padded L^-1) or a :class:`PackedLinv` (read in place);
+    ``z`` (or the PackedLinv's own) is L^-1 w from :func:`predict_z`, which then skips the
+    library's own (``w`` is not read).  Every form gives bit-identical results (gp_predict_ex).
+    """
+    packed = isinstance(chol, PackedLinv)
+    L = chol.buf if packed else chol.linv_buf
+    if z is None and packed:
+        z = chol.z
+    dev = L.device
     X = _as_f64(X, dev, "X")
     Xs = _as_f64(Xs, dev, "Xs")
     n, d = X.shape
     if n != chol.n:
         raise ValueError("X rows do not match the factorisation")
     m = Xs.shape[0]
-    batch = chol.linv_buf.shape[0]
-    npad = chol.linv_buf.shape[1]
+    batch = L.shape[0]
+    npad = padded_n(n)
     beta_t = _beta(beta, batch, d, dev)
     s_t = _per_batch(s, batch, dev, "s")
     sp_t = _per_batch(s_pred, batch, dev, "s_pred")
-    w_t = _as_f64(w, dev, "w")
-    if w_t.dim() == 1:
-        w_t = w_t.reshape(1, -1)
-    if tuple(w_t.shape) != (batch, n):
-        raise ValueError(f"w: expected shape ({batch}, {n}), got {tuple(w_t.shape)}")
+    w_t = None
+    if z is None:
+        w_t = _as_f64(w, dev, "w")
+        if w_t.dim() == 1:
+            w_t = w_t.reshape(1, -1)
+        if tuple(w_t.shape) != (batch, n):
+            raise ValueError(f"w: expected shape ({batch}, {n}), got {tuple(w_t.shape)}")
+    else:
+        z = z.reshape(batch, -1)
+        if z.dtype != F64 or z.device != dev or z.shape[1] < npad or z.stride(1) != 1:
+            raise ValueError(f"z: expected float64 ({batch}, {npad}) rows on {dev}")
     if out is None:
         mean = torch.empty((batch, m), dtype=F64, device=dev)
         var = torch.empty((batch, m), dtype=F64, device=dev)
@@ -216,11 +285,14 @@ def predict(chol: Cholesky, X: torch.Tensor, Xs: torch.Tensor, beta, s, s_pred, 
         mean, var = out
     nbytes = _capi.lib().gp_predict_ws_bytes(n, m, batch, int(m_chunk))
     ws = (workspace or _DEFAULT_WS).get(nbytes, dev)
-    _capi.call("gp_predict", chol.linv_buf.data_ptr(), npad, npad * npad, X.data_ptr(), d,
-               Xs.data_ptr(), d, n, m, d, beta_t.data_ptr(), d, s_t.data_ptr(),
-               sp_t.data_ptr(), w_t.data_ptr(), n, mean.data_ptr(), var.data_ptr(),
-               mean.stride(0) if batch > 1 else m, batch, ws.data_ptr(), ws.numel(),
-               int(m_chunk), _stream(dev))
+    _capi.call("gp_predict_ex", L.data_ptr(), npad, L.stride(0) if packed else npad * npad,
+               X.data_ptr(), d, Xs.data_ptr(), d, n, m, d, beta_t.data_ptr(), d,
+               s_t.data_ptr(), sp_t.data_ptr(), w_t.data_ptr() if w_t is not None else None, n,
+               mean.data_ptr(), var.data_ptr(), mean.stride(0) if batch > 1 else m, batch,
+               ws.data_ptr(), ws.numel(), int(m_chunk),
+               _capi.LINV_PACKED if packed else _capi.LINV_PADDED,
+               z.data_ptr() if z is not None else None,
+               z.stride(0) if z is not None else 0, _stream(dev))
     return mean, var
 
 

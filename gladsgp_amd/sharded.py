@@ -11,9 +11,10 @@ Two ways to get every rank the factor it needs:
 
 * ``mode="redundant"``: every rank builds the Gram and factorises it itself (gp_fit_predict
   on its block; the Amdahl term is the factorisation, ~2 ms of a 27 ms C3 step);
-* ``mode="broadcast"``: rank 0 alone factorises and broadcasts L^-1 (its lower triangle packed,
-  half the bytes of the padded square) while its own block is shortened by the factorisation's
-  time in test-point equivalents (``split_counts``), so all ranks finish together.
+* ``mode="broadcast"``: rank 0 alone factorises and broadcasts L^-1 (tile-packed, half the
+  bytes of the padded square, read by the other ranks' prediction in place) with z = L^-1 w,
+  while its own block is shortened by the factorisation's time in test-point equivalents
+  (``balanced_split``), so all ranks finish together.
 
 :class:`PipelinedPredictor` runs a *stream* of GPs as a two-stage pipeline: in step k rank 0
 factorises GP k+1 and broadcasts its L^-1 (asynchronously over RCCL, double-buffered) while
@@ -56,42 +57,68 @@ def _offsets(counts: list[int]) -> list[int]:
 
 
 class LinvPacker:
-    """L^-1's nonzero part (column c of the column-major buffer from row c on) as one flat
-    vector: what the broadcast carries (about half the padded square), followed by one slot
-    holding the factorisation's info, so every receiver learns whether the factor it got is
-    valid from the same collective (a rank-0-only raise before the broadcast would leave the
-    other ranks waiting in it).  Packed and unpacked by libgpfit (gp_pack_tril /
-    gp_unpack_tril: one coalesced copy each way, no index tensor)."""
+    """The single-GP broadcast's payload, one flat float64 vector:
+    ``[L^-1 tile-packed (elems) | z = L^-1 w (npad) | info (1)]``.
 
-    def __init__(self, npad: int, device):
+    L^-1 travels in the tile-packed layout (gp_pack_linv: column c of the padded buffer from row
+    16 floor(c/16) on, about half the padded square, 67 MB at n = 4096) that the prediction
+    reads in place (gp_predict_ex), so the receiving ranks run no unpack; z is computed once on
+    rank 0 with the prediction's own arithmetic (gp_predict_z), so they run no trmv either
+    (round 4 had every rank >= 1 unpack 134 MB and redo the 71 MB trmv each step).  The info
+    slot carries rank 0's factorisation status, so every receiver learns from the same
+    collective whether the factor it got is valid (a rank-0-only raise before the broadcast
+    would leave the other ranks waiting in it)."""
+
+    def __init__(self, npad: int, device=None, n: int | None = None):
         self.npad = npad
-        self.numel = npad * (npad + 1) // 2
+        self.n = npad if n is None else n
+        q = npad // 16
+        self.elems = npad * npad - 128 * q * (q - 1)      # gp_linv_packed_elems
+        self.numel = self.elems                           # the L^-1 part (round-4 name)
+        self.z_off = self.elems
+        self.info_off = self.elems + npad
 
     def buffer(self, device) -> torch.Tensor:
-        return torch.zeros(self.numel + 1, dtype=F64, device=device)
+        return torch.zeros(self.info_off + 1, dtype=F64, device=device)
 
     @staticmethod
     def order(npad: int) -> torch.Tensor:
-        """The packed layout as flat indices into the column-major (npad x npad) buffer (host
-        tensor; documents gp_pack_tril's order for host-side tests)."""
-        tri = torch.triu_indices(npad, npad)                  # (c, r), r >= c, c-major
-        return tri[0] * npad + tri[1]
+        """The tile-packed layout as flat indices into the column-major (npad x npad) buffer
+        (host tensor; documents gp_pack_linv's order for host-side tests)."""
+        idx = [c * npad + torch.arange((c // 16) * 16, npad) for c in range(npad)]
+        return torch.cat(idx)
 
-    def pack(self, linv_buf: torch.Tensor, info: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-        _capi.call("gp_pack_tril", linv_buf.data_ptr(), self.npad, self.npad, out.data_ptr(),
+    def pack(self, linv_buf: torch.Tensor, info: torch.Tensor, out: torch.Tensor,
+             w: torch.Tensor | None = None) -> torch.Tensor:
+        """Rank 0: L^-1 (padded, (1, npad, npad)) tile-packed, z = L^-1 w (when ``w`` is
+        given) and the info word into ``out``."""
+        _capi.call("gp_pack_linv", linv_buf.data_ptr(), self.n, self.npad, out.data_ptr(),
                    kernels._stream(out.device))
-        out[self.numel:].copy_(info.reshape(1).to(F64))
+        if w is not None:
+            ch = kernels.Cholesky(self.n, None, linv_buf, info, None)
+            kernels.predict_z(ch, w, out=self.z(out).reshape(1, self.npad))
+        out[self.info_off:].copy_(info.reshape(1).to(F64))
         return out
 
     def unpack(self, packed: torch.Tensor, linv_buf: torch.Tensor) -> torch.Tensor:
-        """Into a buffer whose upper triangle and padding are already zero."""
-        _capi.call("gp_unpack_tril", packed.data_ptr(), self.npad, linv_buf.data_ptr(),
+        """Into a padded buffer whose upper triangle and padding are already zero (not needed
+        by the prediction, which reads the packed form in place)."""
+        _capi.call("gp_unpack_linv", packed.data_ptr(), self.n, linv_buf.data_ptr(),
                    self.npad, kernels._stream(packed.device))
         return linv_buf
 
+    def z(self, packed: torch.Tensor) -> torch.Tensor:
+        return packed[self.z_off:self.info_off]
+
     def info(self, packed: torch.Tensor) -> torch.Tensor:
         """The sender's info (device, int32, shape (1,))."""
-        return packed[self.numel:].to(torch.int32)
+        return packed[self.info_off:].to(torch.int32)
+
+    def view(self, packed: torch.Tensor, info: torch.Tensor | None = None) -> kernels.PackedLinv:
+        """The payload as the prediction reads it: tile-packed L^-1 and z, in place."""
+        return kernels.PackedLinv(self.n, packed[: self.elems].view(1, self.elems),
+                                  self.info(packed) if info is None else info,
+                                  self.z(packed).view(1, self.npad))
 
 
 def _wire_bcast(ctx: gdist.Context, t: torch.Tensor, async_op: bool):
@@ -150,25 +177,21 @@ def predict_sharded(ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, beta,
                                 ctx=fctx, check=check)
     else:
         npad = kernels.padded_n(n)
-        linv = torch.zeros((1, npad, npad), dtype=F64, device=dev)
-        info = torch.zeros(1, dtype=torch.int32, device=dev)
-        logdet = torch.zeros(1, dtype=F64, device=dev)
-        packer = LinvPacker(npad, dev)
+        packer = LinvPacker(npad, dev, n=n)
         packed = packer.buffer(dev)
         if rank == 0:
             G = kernels.gram(X, beta, s, delta)
             ch = kernels.cholesky_inverse(G)
-            packer.pack(ch.linv_buf, ch.info, packed)
+            packer.pack(ch.linv_buf, ch.info, packed, w=w)
         _wire_bcast(ctx, packed, async_op=False)
         if check:                                  # every rank raises alike (rank 0's info)
             kernels.check_info(packer.info(packed))
-        if rank != 0:
-            packer.unpack(packed, linv)
-            info.copy_(packer.info(packed))
-            ch = kernels.Cholesky(n, None, linv, info, logdet)
+        # rank 0 from its padded L^-1, the others from the payload in place; z from the payload
+        src = ch if rank == 0 else packer.view(packed)
         if hi > lo:
-            kernels.predict(ch, X, Xl, beta, s, s_pred, w, m_chunk=m_chunk, workspace=workspace,
-                            out=(buf[0:1, : hi - lo], buf[1:2, : hi - lo]))
+            kernels.predict(src, X, Xl, beta, s, s_pred, w, m_chunk=m_chunk, workspace=workspace,
+                            out=(buf[0:1, : hi - lo], buf[1:2, : hi - lo]),
+                            z=packer.z(packed).view(1, npad))
     mine = buf[:, : hi - lo]
     if not gather:
         return mine[0], mine[1], (lo, hi)
@@ -354,10 +377,13 @@ class PipelinedPredictor:
         self.ml = counts[self.rank]
         self.Xl = Xs[lo:lo + self.ml].contiguous()
         npad = kernels.padded_n(self.n)
-        self.linv = [torch.zeros((1, npad, npad), dtype=F64, device=self.dev) for _ in range(2)]
+        self.npad = npad
+        # rank 0 factorises into padded buffers; the other ranks predict from the payload
+        self.linv = [torch.zeros((1, npad, npad), dtype=F64, device=self.dev)
+                     for _ in range(2 if self.rank == 0 else 0)]
         self.info = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.logdet = torch.zeros(1, dtype=F64, device=self.dev)
-        self.packer = LinvPacker(npad, self.dev)
+        self.packer = LinvPacker(npad, self.dev, n=self.n)
         self.packed = [self.packer.buffer(self.dev) for _ in range(2)]
         # the first nonzero info among the GPs predicted so far (device; read by check())
         self.status = torch.zeros(1, dtype=torch.int32, device=self.dev)
@@ -396,7 +422,9 @@ class PipelinedPredictor:
 
     def _bcast(self, slot: int):
         if self.rank == 0:
-            self.packer.pack(self.linv[slot], self.info, self.packed[slot])
+            # L^-1 tile-packed + z = L^-1 w of this GP's w + info
+            self.packer.pack(self.linv[slot], self.info, self.packed[slot],
+                             w=self.gps[slot][4])
         if not self.dist:
             return None
         return _wire_bcast(self.ctx, self.packed[slot], async_op=True)
@@ -422,16 +450,18 @@ class PipelinedPredictor:
             nxt_req = self._bcast(nxt)
         if self.pending is not None:
             self.pending.wait()
-        if self.rank != 0:
-            self.packer.unpack(self.packed[cur], self.linv[cur])
         got = self.packer.info(self.packed[cur])
         self.status.copy_(torch.where(self.status != 0, self.status, got))
         b, s, _, sp, w = self.gps[cur]
-        ch = kernels.Cholesky(self.n, None, self.linv[cur], self.info, self.logdet)
+        # rank 0 predicts from its padded L^-1, every other rank from the payload in place (no
+        # unpack); all of them with the shipped z (no trmv)
+        ch = (kernels.Cholesky(self.n, None, self.linv[cur], self.info, self.logdet)
+              if self.rank == 0 else self.packer.view(self.packed[cur], self.info))
         if self.ml:
             kernels.predict(ch, self.X, self.Xl, b, s, sp, w, m_chunk=self.m_chunk,
                             workspace=self.ws, out=(self.out[0:1, : self.ml],
-                                                    self.out[1:2, : self.ml]))
+                                                    self.out[1:2, : self.ml]),
+                            z=self.packer.z(self.packed[cur]).view(1, self.npad))
         if not self.dist:
             res = self.out[:, : self.ml]
         elif self.ctx.backend == "nccl":

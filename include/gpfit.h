@@ -145,6 +145,48 @@ int gp_predict(const double* Linv, int ldinv, long long strideInv,
                int batch, void* ws, long long ws_bytes, int m_chunk, hipStream_t stream);
 
 /*
+ * gp_predict with the L^-1 layout and z = L^-1 w as options (the sharded single-GP path,
+ * ranks >= 1 predict straight from the broadcast payload, no unpack and no trmv):
+ *   layout GPFIT_LINV_PADDED: Linv as gp_predict (column k at Linv + k*ldinv);
+ *   layout GPFIT_LINV_PACKED: Linv tile-packed (gp_pack_linv), ldinv ignored, strideInv >=
+ *          gp_linv_packed_elems(n) between problems;
+ *   z != NULL: z_b = z + b*ldz (gp_padded_n(n) values, from gp_predict_z) is used as L^-1 w and
+ *          w_hat is not read; z == NULL: computed as gp_predict does.
+ * Results are bit-identical to gp_predict's for every layout and z option.  Argument numbers
+ * 1-23 as gp_predict; -24 layout, -26 ldz.  Workspace: gp_predict_ws_bytes.
+ */
+#define GPFIT_LINV_PADDED 0
+#define GPFIT_LINV_PACKED 1
+int gp_predict_ex(const double* Linv, int ldinv, long long strideInv,
+                  const double* X, int ldx, const double* Xs, int ldxs, int n, int m, int d,
+                  const double* beta, int ldbeta, const double* s, const double* s_pred,
+                  const double* w_hat, int ldw, double* mean, double* var, int ldo,
+                  int batch, void* ws, long long ws_bytes, int m_chunk, int layout,
+                  const double* z, long long ldz, hipStream_t stream);
+
+/*
+ * z_b = Linv_b w_b (gp_padded_n(n) rows, zero past n) with exactly the arithmetic gp_predict
+ * applies internally, into z + b*ldz: what rank 0 ships with L^-1 so the other ranks skip it.
+ * `ws` holds gp_predict_z_ws_bytes(n, batch) bytes.  layout as gp_predict_ex.
+ */
+long long gp_predict_z_ws_bytes(int n, int batch);
+int gp_predict_z(const double* Linv, int ldinv, long long strideInv, int layout, int n,
+                 const double* w_hat, int ldw, double* z, long long ldz, int batch, void* ws,
+                 long long ws_bytes, hipStream_t stream);
+
+/*
+ * The tile-packed L^-1: column c of the padded buffer from row 16*floor(c/16) on (every stored
+ * run starts on a 16-row tile and is a multiple of 16 doubles, so the prediction's 16-B loads
+ * and 16-row MFMA tiles read it in place), columns one after another:
+ * gp_linv_packed_elems(n) = npad^2 - 128 q (q - 1) doubles, q = npad / 16, npad =
+ * gp_padded_n(n) -- about half the padded square (67 MB at n = 4096).  Both buffers 16-B
+ * aligned; gp_unpack_linv writes only the stored elements.
+ */
+long long gp_linv_packed_elems(int n);
+int gp_pack_linv(const double* Linv, int n, int ldinv, double* P, hipStream_t stream);
+int gp_unpack_linv(const double* P, int n, double* Linv, int ldinv, hipStream_t stream);
+
+/*
  * gp_predict from the Cholesky factor L itself (the §8b form, LAPACK layout, lower): L^-1 by
  * gp_trtri into the head of `ws`, then gp_predict.  `ws` holds
  * gp_predict_chol_ws_bytes(n, m, batch, m_chunk) bytes; info as gp_trtri (mean / var of a

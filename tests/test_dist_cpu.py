@@ -139,22 +139,26 @@ def _points_worker(rank, world, port, results):
             ok_p = bool(torch.equal(out[0], ref) and torch.equal(out[1], -ref))
         else:
             ok_p = out is None
-        # L^-1 broadcast packed to its lower triangle (sharded.LinvPacker), rebuilt exactly
-        npad = 8
+        # L^-1 broadcast tile-packed (sharded.LinvPacker: column c from row 16 floor(c/16) on),
+        # with z and rank 0's factorisation info, so every rank can raise alike; rebuilt exactly
+        # (gp_pack_linv / gp_unpack_linv run on the GPU; here the documented layout, host-side)
+        npad = 128
         full = torch.tril(torch.arange(1.0, npad * npad + 1, dtype=torch.float64)
                           .reshape(npad, npad)).T.contiguous().reshape(1, npad, npad)
-        # together with rank 0's factorisation info, so every rank can raise alike
-        # (gp_pack_tril / gp_unpack_tril run on the GPU; here the documented layout, host-side)
         pk = LinvPacker(npad, torch.device("cpu"))
         order = LinvPacker.order(npad)
         packed = pk.buffer(torch.device("cpu"))
+        zz = torch.arange(npad, dtype=torch.float64) * 0.5
         if rank == 0:
-            packed[: pk.numel] = full.reshape(-1)[order]
-            packed[pk.numel:] = 3.0
+            packed[: pk.elems] = full.reshape(-1)[order]
+            pk.z(packed).copy_(zz)
+            packed[pk.info_off:] = 3.0
         gdist.broadcast_(ctx, packed)
         got = torch.zeros((1, npad, npad), dtype=torch.float64)
-        got.view(-1).index_copy_(0, order, packed[: pk.numel])
-        ok_l = (bool(torch.equal(got, full)) and pk.numel == npad * (npad + 1) // 2
+        got.view(-1).index_copy_(0, order, packed[: pk.elems])
+        q = npad // 16
+        ok_l = (bool(torch.equal(got, full)) and pk.elems == npad * npad - 128 * q * (q - 1)
+                and order.numel() == pk.elems and bool(torch.equal(pk.z(packed), zz))
                 and pk.info(packed).tolist() == [3])
         results[rank] = (ok_p, ok_l)
     finally:

@@ -75,3 +75,51 @@ def test_schedule_bit_identical_across_chunkings_and_paths(dev, n, m, B):
         assert np.max(np.abs(ref_m[b, idx] - mr)) <= 1e-8 * max(1.0, np.max(np.abs(mr))), b
         assert np.max(np.abs(ref_v[b, idx] - vr)) <= 1e-9 * s[b], b
 
+
+
+@pytest.mark.parametrize("n,B", [(5, 1), (300, 2), (1000, 1), (4096, 1)])
+def test_packed_linv_and_shipped_z_bit_identical(dev, n, B):
+    """The sharded single-GP path's payload (sharded.LinvPacker): L^-1 tile-packed
+    (gp_pack_linv, read in place by the TRMM and the trmv of gp_predict_ex) and z = L^-1 w from
+    gp_predict_z give the padded path's answers bit for bit; the packed layout round-trips
+    (gp_unpack_linv) and matches LinvPacker.order (host-documented layout)."""
+    from gladsgp_amd import kernels
+    from gladsgp_amd.sharded import LinvPacker
+    m = 3000 if n < 4096 else 20000
+    X, Xs, betas, W, s, delta = _problem(n, m, B, 7 * n + B)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+    Xd, Xsd, bd, Wd, sd, dd = t(X), t(Xs), t(betas), t(W), t(s), t(delta)
+    ch = kernels.cholesky_inverse(kernels.gram(Xd, bd, sd, dd, batch=B))
+    ch.check()
+    npad = kernels.padded_n(n)
+    ref_m, ref_v = kernels.predict(ch, Xd, Xsd, bd, sd, sd, Wd)
+    P = kernels.pack_linv(ch)
+    assert P.shape == (B, kernels.linv_packed_elems(n))
+    order = LinvPacker.order(npad).to(dev)
+    for b in range(B):
+        assert torch.equal(P[b], ch.linv_buf[b].reshape(-1)[order])
+    z = kernels.predict_z(ch, Wd)
+    pk = kernels.PackedLinv(n, P, ch.info)
+    assert torch.equal(kernels.predict_z(pk, Wd), z)
+    assert torch.all(z[:, n:] == 0)
+    for name, (src, zz) in {"padded+z": (ch, z), "packed": (pk, None),
+                            "packed+z": (pk, z)}.items():
+        mu, var = kernels.predict(src, Xd, Xsd, bd, sd, sd, None if zz is not None else Wd, z=zz)
+        assert torch.equal(mu, ref_m) and torch.equal(var, ref_v), name
+    # chunked and merged-tail paths read the packed layout alike
+    mu, var = kernels.predict(pk, Xd, Xsd, bd, sd, sd, Wd, m_chunk=1280)
+    assert torch.equal(mu, ref_m) and torch.equal(var, ref_v)
+    back = torch.zeros_like(ch.linv_buf)
+    from gladsgp_amd import _capi
+    for b in range(B):
+        _capi.call("gp_unpack_linv", P[b].data_ptr(), n, back[b].data_ptr(), npad,
+                   kernels._stream(dev))
+    assert torch.equal(back, ch.linv_buf)
+    # the payload as the pipelined predictor ships it (B = 1)
+    if B == 1:
+        packer = LinvPacker(npad, dev, n=n)
+        buf = packer.buffer(dev)
+        packer.pack(ch.linv_buf, ch.info, buf, w=Wd)
+        assert torch.equal(packer.z(buf), z[0]) and packer.info(buf).tolist() == [0]
+        mu, var = kernels.predict(packer.view(buf), Xd, Xsd, bd, sd, sd, None)
+        assert torch.equal(mu, ref_m) and torch.equal(var, ref_v)
