@@ -8,14 +8,15 @@
 A step is one full pass of the hot path for one GP, from hyperparameters to answers on rank 0:
 ARD-SE Gram (n x n) -> blocked MFMA Cholesky + L^-1 -> cross-covariance / TRMM / mean+variance
 over the test points.  Inside a step the cross-covariance (independent of the factorisation)
-runs on the caller-owned context's CU-masked stream while the latency-bound Cholesky runs
+runs on the caller-owned context's own stream beside the latency-bound factorisation
 (``--serial``: no context, every kernel in order on one stream).  Inputs are HBM-resident
 before the timed region.
 
 Multi-GPU (single-output GP): *strong scaling* of the fixed m = 100k test points
 over a stream of GPs.  The headline at N > 1 is a two-stage pipeline (``c3_pipelined``): in step k
-rank 0 builds GP k+1's Gram and L, L^-1 and broadcasts L^-1 (RCCL, async, packed to the lower triangle, double-buffered)
-while every rank predicts GP k on its block of the test points, and each step ends with one
+rank 0 builds GP k+1's Gram and L, L^-1 and broadcasts L^-1 (RCCL, async, tile-packed, with
+z = L^-1 w, double-buffered; the other ranks predict from it in place) while every rank
+predicts GP k on its block of the test points, and each step ends with one
 gather of the (mean, var) blocks to rank 0 (inside the timed region).  Rank 0's block is
 shortened by the factorisation's measured time, consecutive GPs have different
 hyperparameters, and the last step is checked against a direct computation.  Beside it
@@ -144,15 +145,17 @@ def cpu_baseline(X, y, beta, Xs, s, delta, sample: int = 20000, reps: int = 3,
     t_one = f1 + p1 / s1 * m
     # "reference-faithful": re-factorise per batch of 4 points (assess_all_models.py:481-489)
     nb = max(1, min(faithful_batches, m // 4))
-    t2 = time.perf_counter()
+    tb = []
     for k in range(nb):
+        t2 = time.perf_counter()
         xb = Xs[4 * k:4 * k + 4]
         G4 = gp_ref.gram_ardse(X, beta, s, delta)
         L4 = np.linalg.cholesky(G4)
         a4 = sla.cho_solve((L4, True), y)
         K4 = gp_ref.cross_ardse(xb, X, beta, s)
         _ = K4 @ a4, sla.solve_triangular(L4, K4.T, lower=True)
-    t4 = time.perf_counter() - t2
+        tb.append(time.perf_counter() - t2)
+    t4 = float(np.sum(tb))
     aff = len(os.sched_getaffinity(0))
     return {
         "value": m / t_full, "unit": "predictions/s", "cores": _CPU_THREADS, "kind": "port",
@@ -167,10 +170,17 @@ def cpu_baseline(X, y, beta, Xs, s, delta, sample: int = 20000, reps: int = 3,
                                  f"{f1:.2f} s + predict {p1:.2f} s for {s1} points, "
                                  f"extrapolated to m={m}"),
         "reference_faithful_value": 4.0 * nb / t4,
+        "reference_faithful_batch_s": {"min": float(np.min(tb)), "median": float(np.median(tb)),
+                                       "max": float(np.max(tb)), "batches": nb},
         "reference_faithful_sample": (f"re-factorise per batch of 4 test points as "
                                       f"assess_all_models.py:481-489 does: {nb} batches "
-                                      f"({4 * nb} test points) timed, {t4:.2f} s, "
-                                      f"{_CPU_THREADS} threads"),
+                                      f"({4 * nb} test points) timed, {t4:.2f} s in all, per "
+                                      f"batch min {np.min(tb):.3f} / median "
+                                      f"{np.median(tb):.3f} / max {np.max(tb):.3f} s, "
+                                      f"{_CPU_THREADS} threads; the rate is per batch (every "
+                                      "batch does one full n x n Gram + factorisation, so "
+                                      "it extrapolates linearly in the batches: 400 points "
+                                      "(the assess_all_models subset) = 100 batches)"),
     }, np.concatenate(means), np.concatenate(vars_)
 
 
@@ -509,14 +519,16 @@ def main():
         line["ms_per_step"] = pipe["elapsed"] / K * 1e3
         line["config"]["parallelism"] = (
             f"pipelined x{ctx.world}: rank 0 builds GP k+1's Gram + L, L^-1 and broadcasts L^-1 "
-            "(RCCL, async, packed to the lower triangle, double-buffered) while every rank predicts GP k on its test-point "
-            "block and the blocks are gathered to rank 0; rank 0's block shortened by the "
+            "(RCCL, async, tile-packed with z = L^-1 w, double-buffered) while every rank "
+            "predicts GP k on its test-point block (ranks >= 1 straight from the payload) and "
+            "the blocks are gathered to rank 0; rank 0's block shortened by the "
             "factorisation's time")
         line["config"]["m_test_per_rank"] = pipe["counts"]
         line["config"]["m_test_rank0"] = pipe["counts"][0]
-        line["config"]["pipeline"] = ("per rank: gp_predict (cross-covariance, TRMM, mean/var) "
-                                      "from the broadcast L^-1; rank 0 also gp_gram_ardse + "
-                                      "gp_potrf_inv of the next GP, first")
+        line["config"]["pipeline"] = ("per rank: gp_predict_ex (cross-covariance, TRMM, "
+                                      "mean/var) from the broadcast tile-packed L^-1 and z; "
+                                      "rank 0 also gp_gram_ardse + gp_potrf_inv + gp_pack_linv "
+                                      "+ gp_predict_z of the next GP, first")
         line["pipeline"] = {"t_fact_ms": pipe["t_fact_ms"], "t_point_us": pipe["t_point_us"],
                             "check_last_step_vs_direct": pipe["check"]}
     if ctx.world == 1 and not args.no_cpu:
@@ -638,7 +650,37 @@ def main_c4(args):
         "cpu_baseline": None,
     }
     assert out is not None and out[0].shape == (P, m)
+    if ctx.world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_c4(X, W, beta, Xs, s, delta, out)
     print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_c4(X, W, beta, Xs, s, delta, out, pcs: int = 2, sample: int = 2000):
+    """The numpy fp64 oracle on the host for C4: ``pcs`` of the PC GPs, each a full n = 1024
+    Gram + Cholesky + alpha and the first ``sample`` test points (gp_ref's chunked
+    cross-covariance / solve_triangular), extrapolated linearly in the points to m and in the
+    PCs to P (the PCs are independent problems of one shape); the GPU's answers for those
+    points are checked against it."""
+    P, m = W.shape[0], Xs.shape[0]
+    per_pc, dm, dv = [], 0.0, 0.0
+    for j in range(pcs):
+        t_fact, t_pred, means, vars_ = _cpu_c3_run(X, W[j], beta[j], Xs, float(s[j]),
+                                                   float(delta[j]), sample)
+        per_pc.append(t_fact + t_pred / sample * m)
+        mu_g = out[0][j, :sample].cpu().numpy()
+        var_g = out[1][j, :sample].cpu().numpy()
+        dm = max(dm, float(np.max(np.abs(mu_g - np.concatenate(means)))))
+        dv = max(dv, float(np.max(np.abs(var_g - np.concatenate(vars_)))))
+    t_all = float(np.mean(per_pc)) * P
+    return {"value": P * m / t_all, "unit": "predictions/s", "cores": _CPU_THREADS,
+            "kind": "port",
+            "sample": (f"oracle/gp_ref numpy fp64, OpenBLAS {_CPU_THREADS} threads on "
+                       f"{cpu_model()}: {pcs} of the {P} PC GPs, each the full n={X.shape[0]} "
+                       f"Gram + Cholesky + predict of the first {sample} of {m} test points "
+                       f"({', '.join(f'{t:.2f}' for t in per_pc)} s per PC extrapolated to "
+                       f"m), extrapolated to {P} PCs"),
+            "parity_vs_gpu": {"pcs": pcs, "points": sample, "max_abs_dmean": dm,
+                              "max_abs_dvar": dv}}
 
 
 def synthetic_field(n: int, d: int, ny: int, seed: int = 0):

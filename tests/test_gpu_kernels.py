@@ -542,8 +542,9 @@ def test_cholesky_grid_gram_ill_conditioned(dev, n, ell):
 
 @pytest.mark.parametrize("n,ld", [(1, 1), (7, 9), (128, 128), (1000, 1024)])
 def test_pack_unpack_tril_round_trip(dev, n, ld):
-    """gp_pack_tril / gp_unpack_tril (the single-GP broadcast's payload): column c from row c
-    on, column after column; unpacking writes the lower triangle only."""
+    """gp_pack_tril / gp_unpack_tril (the round-4 single-GP broadcast payload, kept as a plain
+    lower-triangle utility; the payload is now the tile-packed layout, test_gpu_sched.py):
+    column c from row c on, column after column; unpacking writes the lower triangle only."""
     from gladsgp_amd import _capi
     rng = np.random.default_rng(n)
     A = rng.standard_normal((n, ld))                       # [col][row] = column-major, ld rows
@@ -553,9 +554,6 @@ def test_pack_unpack_tril_round_trip(dev, n, ld):
     _capi.call("gp_pack_tril", At.data_ptr(), n, ld, v.data_ptr(), st)
     ref = np.concatenate([A[c, c:n] for c in range(n)])
     assert np.array_equal(v.cpu().numpy(), ref)
-    if ld == n:                                            # sharded.LinvPacker's order
-        from gladsgp_amd.sharded import LinvPacker
-        assert np.array_equal(A.reshape(-1)[LinvPacker.order(n).numpy()], ref)
     B = torch.full((n, ld), 7.0, dtype=torch.float64, device=dev)
     _capi.call("gp_unpack_tril", v.data_ptr(), n, B.data_ptr(), ld, st)
     Bh = B.cpu().numpy()
