@@ -443,7 +443,8 @@ hipError_t cross_kp_launch(const double* X, int n, int ldx, const double* Xs, in
 //   pass 1: block (rb, s) forms row block rb's kZR rows (2 per thread, one 16-B load per
 //           column) times column strip s (kZS columns; strips right of the row block are zero
 //           and skipped: 288 blocks at n = 4096), k ascending, into zp[s][r];
-//   pass 2: z[r] = sum over s = 0 .. last strip of r's row block of zp[s][r], in strip order.
+//   pass 2: z[r] = the sum over s = 0 .. last strip of r's row block of zp[s][r], as eight
+//           in-order runs of strips combined in a fixed tree (trmv_sum_kernel).
 // Every row r < npad is written (rows >= n are 0: L^-1 is zero-padded).  zp (batch *
 // ceil(npad / kZS) * npad doubles, 2 MB per problem at n = 4096) is its own workspace region.
 constexpr int kZR = 512;   // rows per pass-1 block
@@ -489,17 +490,30 @@ __global__ __launch_bounds__(256) void trmv_part_kernel(const double* __restrict
       make_double2(a0, a1);
 }
 
+// Pass 2: 32 rows per block, 8 threads per row, thread g summing its row's strips
+// g * per .. (g + 1) * per - 1 in order, the 8 partials combined in a fixed tree (one thread per
+// row summing all 64 strips serially took 23 us at n = 4096, this 6 us:
+// tools/dbg/trmv_micro.hip, profiles/r05/r05b_trmv_micro.log).
 __global__ __launch_bounds__(256) void trmv_sum_kernel(const double* __restrict__ zp, int nst,
                                                        int npad, int n, double* __restrict__ z,
                                                        long long ldz) {
-  const int b = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= npad) return;
-  const int rb = (r / kZR) * kZR;
-  const int last = min(rb + kZR - 1, n - 1) / kZS;  // pass 1's strips for r's row block
-  const double* q = zp + (long long)b * nst * npad + r;
+  __shared__ double red[8][32];
+  const int b = blockIdx.y, rl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int r = blockIdx.x * 32 + rl;
   double acc = 0.0;
-  for (int s = 0; s <= last; ++s) acc += q[(long long)s * npad];
-  z[(long long)b * ldz + r] = acc;
+  if (r < npad) {
+    const int rb = (r / kZR) * kZR;
+    const int cnt = min(rb + kZR - 1, n - 1) / kZS + 1;   // pass 1's strips for r's row block
+    const int per = (cnt + 7) / 8;
+    const int s0 = g * per, s1 = min(cnt, s0 + per);
+    const double* q = zp + (long long)b * nst * npad + r;
+    for (int s = s0; s < s1; ++s) acc += q[(long long)s * npad];
+  }
+  red[g][rl] = acc;
+  __syncthreads();
+  if (g == 0 && r < npad)
+    z[(long long)b * ldz + r] = ((red[0][rl] + red[1][rl]) + (red[2][rl] + red[3][rl])) +
+                                ((red[4][rl] + red[5][rl]) + (red[6][rl] + red[7][rl]));
 }
 
 struct Plan {
@@ -646,7 +660,7 @@ hipError_t trmv_pred(int npad, double* zp, const LinvRef& L, const double* w_hat
                        w_hat, ldw, zp, npad, n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(trmv_sum_kernel, dim3(gp_ceil_div(npad, 256), batch), dim3(256), 0,
+  hipLaunchKernelGGL(trmv_sum_kernel, dim3(gp_ceil_div(npad, 32), batch), dim3(256), 0,
                      stream, zp, nst, npad, n, z, zld);
   return hipGetLastError();
 }

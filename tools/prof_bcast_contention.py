@@ -4,10 +4,10 @@ packed L^-1 (67 MB at n = 4096) on RCCL's own stream.  A one-GPU box has no peer
 broadcast is a stand-in (tools/dbg/bcast_standin.hip): `wgs` workgroups copying 67 MB on a
 second stream, either unthrottled (HBM-speed) or throttled to last about as long as an xGMI
 transfer (target durations below).  Printed per configuration: the prediction's time (HIP
-events on its stream, gp_predict: trmv + cross-covariance + TRMM + finalize) alone and beside
+events on its stream, gp_predict_ex from the payload: cross-covariance + TRMM + finalize) alone and beside
 the copy, and the copy's own completion time alone and beside the prediction; plus the
-per-step extras of the N > 1 path measured alone: gp_pack_tril (rank 0), gp_unpack_tril (ranks
->= 1, the round-4 path) and the (mean, var) gather stand-in.
+per-step extras of the N > 1 path measured alone: the payload's pack + z (rank 0), the unpack
+the ranks > 0 no longer run, and the (mean, var) gather stand-in.
 
     python tools/prof_bcast_contention.py [points]
 """
@@ -44,7 +44,7 @@ w = torch.as_tensor(np.sin(rng.random(n) * 6), device=dev).reshape(1, n)
 ch = kernels.cholesky_inverse(kernels.gram(X, beta, 1.0, 1e-6))
 ch.check()
 npad = kernels.padded_n(n)
-packer = LinvPacker(npad, dev)
+packer = LinvPacker(npad, dev, n=n)
 nbytes = (packer.numel * 8 + 15) // 16 * 16
 src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
 dst = torch.empty_like(src)
@@ -59,8 +59,14 @@ def ev():
     return torch.cuda.Event(enable_timing=True)
 
 
+payload = packer.buffer(dev)
+packer.pack(ch.linv_buf, ch.info, payload, w=w)
+view = packer.view(payload)
+
+
 def predict():
-    kernels.predict(ch, X, Xs, beta, 1.0, 1.0, w, workspace=ws, out=out)
+    # a rank > 0's step: straight from the broadcast payload (tile-packed L^-1 + z)
+    kernels.predict(view, X, Xs, beta, 1.0, 1.0, None, workspace=ws, out=out)
 
 
 def copy(wgs, sl):
@@ -93,14 +99,15 @@ def run(wgs=None, sl=0, do_pred=True, reps=5):
     return med(tp), med(tc)
 
 
-base, _ = run()
+# warm the clocks, then every configuration between two runs of the prediction alone (clock
+# and power state drift between runs is as large as the effect measured)
+for _ in range(3):
+    run(reps=3)
+base, _ = run(reps=7)
 print(f"prediction of {pts} points at n = {n} alone: {base:.3f} ms", flush=True)
-# calibrate sleep counts so the copy alone lasts ~0.7 / 1.4 ms (xGMI-like: 67 MB at ~96 / 48 GB/s)
+worst = 0.0
 for wgs in (16, 32, 64):
-    _, c0 = run(wgs, 0, do_pred=False)
-    p0, cp0 = run(wgs, 0)
-    print(f"  wgs {wgs:3d} unthrottled: copy alone {c0:.3f} ms; beside: prediction {p0:.3f} ms "
-          f"({p0 / base - 1:+.1%}), copy {cp0:.3f} ms", flush=True)
+    cfgs = [(0, None)]
     for target in (0.7, 1.4):
         sl, c = 1, 0.0
         while sl < 4096:
@@ -108,15 +115,27 @@ for wgs in (16, 32, 64):
             if c >= target:
                 break
             sl *= 2
-        p, cp = run(wgs, sl)
-        print(f"  wgs {wgs:3d} throttled (sleep {sl:4d}, copy alone {c:.3f} ms): prediction "
-              f"{p:.3f} ms ({p / base - 1:+.1%}), copy beside {cp:.3f} ms", flush=True)
+        cfgs.append((sl, c))
+    for sl, c in cfgs:
+        if c is None:
+            _, c = run(wgs, 0, do_pred=False)
+        a0, _ = run(reps=7)
+        p, cp = run(wgs, sl, reps=7)
+        a1, _ = run(reps=7)
+        ratio = p / (0.5 * (a0 + a1))
+        worst = max(worst, ratio)
+        print(f"  wgs {wgs:3d} {'unthrottled' if sl == 0 else f'sleep {sl:4d}'}: copy alone "
+              f"{c:.3f} ms, beside the prediction {cp:.3f} ms; prediction {p:.3f} ms beside vs "
+              f"{a0:.3f} / {a1:.3f} alone before / after: x{ratio:.3f}", flush=True)
+print(f"worst prediction slowdown beside the stand-in broadcast: x{worst:.3f}", flush=True)
 
 # the per-step extras of the N > 1 path
 linv = torch.zeros((1, npad, npad), dtype=torch.float64, device=dev)
 packed = packer.buffer(dev)
-for name, fn in (("gp_pack_tril (rank 0)", lambda: packer.pack(ch.linv_buf, ch.info, packed)),
-                 ("gp_unpack_tril (ranks >= 1, round-4 path)",
+for name, fn in (("gp_pack_linv + gp_predict_z (rank 0, round-5 payload)",
+                  lambda: packer.pack(ch.linv_buf, ch.info, packed, w=w)),
+                 ("gp_pack_linv alone", lambda: packer.pack(ch.linv_buf, ch.info, packed)),
+                 ("gp_unpack_linv (not run any more: ranks >= 1 read the payload in place)",
                   lambda: packer.unpack(packed, linv)),
                  ("gather stand-in (2 x 8 B x points, D2D)",
                   lambda: out[0].copy_(out[1]))):
