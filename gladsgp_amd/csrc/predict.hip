@@ -272,10 +272,14 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
 
   auto issue = [&](const double* L, int s, double* st) {
     const int k0 = s * BK;
+    // tile-packed: the step's 16 columns share their first stored row 16 s, so column k0 + kr
+    // starts at linv_col(k0) + kr (npad - 16 s) (one multiply per row instead of linv_col's)
+    const long long pbase = PACKED ? linv_col(k0, a.npad) : 0;
+    const int pstride = PACKED ? a.npad - BK * s : 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {              // A rows k0 + 4w + r
       const int kr = 4 * w + r;
-      const long long col = PACKED ? linv_col(k0 + kr, a.npad) : (long long)(k0 + kr) * ld;
+      const long long col = PACKED ? pbase + kr * pstride : (long long)(k0 + kr) * ld;
       glds16(L + col, st + kr * APITCH);
     }
 #pragma unroll
