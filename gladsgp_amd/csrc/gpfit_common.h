@@ -127,6 +127,48 @@ GP_DEV double exp_neg(double a) {
   return fma(a, 0.0, __builtin_ldexp(p, (int)k));
 }
 
+// exp(-a) from a 64-entry table (the prediction's cross-covariance, predict.hip): with
+// q = rint(-a 64 / ln2), exp(-a) = 2^(q >> 6) T[q & 63] exp(r), T[j] = 2^(j / 64) correctly
+// rounded (kExp2Tab), r = -a - q ln2 / 64 (two-part constant), |r| <= ln2 / 128, exp(r) - 1 by
+// its degree-5 Taylor polynomial (truncation 3.5e-17 relative) and T + T (exp(r) - 1) by one
+// fma: within 1 ulp of ocml's exp (tools/dbg/cross_micro.hip: max 1.0 ulp over 67M values),
+// 12 fp64 operations instead of exp_neg's 17 -- the cross-covariance of a batch is bound by its
+// fp64 VALU work (C4 chunk 596 -> 472 us, profiles/r05/r05e_cross_micro.log).  `tab` is an
+// LDS copy of kExp2Tab (per-lane indices).  NaN / Inf arguments propagate as in exp_neg.
+static __constant__ double kExp2Tab[64] = {
+    0x1.0000000000000p+0, 0x1.02c9a3e778061p+0, 0x1.059b0d3158574p+0, 0x1.0874518759bc8p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0e3ec32d3d1a2p+0, 0x1.11301d0125b51p+0, 0x1.1429aaea92de0p+0,
+    0x1.172b83c7d517bp+0, 0x1.1a35beb6fcb75p+0, 0x1.1d4873168b9aap+0, 0x1.2063b88628cd6p+0,
+    0x1.2387a6e756238p+0, 0x1.26b4565e27cddp+0, 0x1.29e9df51fdee1p+0, 0x1.2d285a6e4030bp+0,
+    0x1.306fe0a31b715p+0, 0x1.33c08b26416ffp+0, 0x1.371a7373aa9cbp+0, 0x1.3a7db34e59ff7p+0,
+    0x1.3dea64c123422p+0, 0x1.4160a21f72e2ap+0, 0x1.44e086061892dp+0, 0x1.486a2b5c13cd0p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4f9b2769d2ca7p+0, 0x1.5342b569d4f82p+0, 0x1.56f4736b527dap+0,
+    0x1.5ab07dd485429p+0, 0x1.5e76f15ad2148p+0, 0x1.6247eb03a5585p+0, 0x1.6623882552225p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6dfb23c651a2fp+0, 0x1.71f75e8ec5f74p+0, 0x1.75feb564267c9p+0,
+    0x1.7a11473eb0187p+0, 0x1.7e2f336cf4e62p+0, 0x1.82589994cce13p+0, 0x1.868d99b4492edp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8f1ae99157736p+0, 0x1.93737b0cdc5e5p+0, 0x1.97d829fde4e50p+0,
+    0x1.9c49182a3f090p+0, 0x1.a0c667b5de565p+0, 0x1.a5503b23e255dp+0, 0x1.a9e6b5579fdbfp+0,
+    0x1.ae89f995ad3adp+0, 0x1.b33a2b84f15fbp+0, 0x1.b7f76f2fb5e47p+0, 0x1.bcc1e904bc1d2p+0,
+    0x1.c199bdd85529cp+0, 0x1.c67f12e57d14bp+0, 0x1.cb720dcef9069p+0, 0x1.d072d4a07897cp+0,
+    0x1.d5818dcfba487p+0, 0x1.da9e603db3285p+0, 0x1.dfc97337b9b5fp+0, 0x1.e502ee78b3ff6p+0,
+    0x1.ea4afa2a490dap+0, 0x1.efa1bee615a27p+0, 0x1.f50765b6e4540p+0, 0x1.fa7c1819e90d8p+0,
+};
+
+GP_DEV double exp_neg_tab(double a, const double* tab) {
+  const double x = -fmin(a, 1100.0);
+  const double q = __builtin_rint(x * 0x1.71547652b82fep+6);               // x 64 / ln2
+  double r = fma(q, -0x1.62e42fefa39efp-7, x);                             // - q ln2/64 (hi)
+  r = fma(q, -0x1.abc9e3b39803fp-62, r);                                   // - q ln2/64 (lo)
+  double p = fma_sc(r, 0x1.1111111111111p-7, 0x1.5555555555555p-5);        // 1/120, 1/24
+  p = fma_sc(p, r, 0x1.5555555555555p-3);                                  // 1/6
+  p = fma_sc(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = p * r;                                                               // exp(r) - 1
+  const int qi = (int)q;
+  const double t = tab[qi & 63];
+  return fma(a, 0.0, __builtin_ldexp(fma(t, p, t), qi >> 6));
+}
+
 // Squared ARD distance sum_k beta_k (a_k - b_k)^2 ; D is a compile-time dimension bound.
 template <int D>
 GP_DEV double ard_dist(const double* __restrict__ a, const double* __restrict__ b,

@@ -37,6 +37,7 @@ constexpr int kDefaultChunkSingle = 16384;            // ... and for one GP
 
 // Cross-covariance chunk, k-major as the TRMM streams it:
 //   Kt[k * mc + c] = s * exp(-sum beta (X[k] - Xs[c])^2)
+// (exp by the 64-entry table, exp_neg_tab: the kernel is bound by its fp64 VALU work)
 // (zero for k >= n or c >= mv).  Each thread owns one test point c (registers) and walks 32
 // k-pairs whose design rows are broadcast from LDS; a wave stores 512 contiguous bytes per
 // row k.  Both design vectors are pre-scaled by sqrt(beta) (beta >= 0): 2 d ops per element
@@ -51,8 +52,10 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
   const int kp0 = blockIdx.y * 32;
   __shared__ double xk[64][D];
   __shared__ double bs[D];
+  __shared__ double tab[64];
   const double* bb = beta + (long long)b * ldbeta;
   if (threadIdx.x < D) bs[threadIdx.x] = (threadIdx.x < d) ? __builtin_sqrt(bb[threadIdx.x]) : 0.0;
+  if (threadIdx.x < 64) tab[threadIdx.x] = kExp2Tab[threadIdx.x];
   __syncthreads();
   for (int t = threadIdx.x; t < 64 * D; t += 256) {
     const int kk = t / D, dd = t % D, k = 2 * kp0 + kk;
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
     }
     // exp unconditionally, then select: padding rows / columns have finite (zeroed) inputs,
     // and a conditional exp costs an exec-mask branch around each call
-    const double v0 = sb * exp_neg(e0), v1 = sb * exp_neg(e1);
+    const double v0 = sb * exp_neg_tab(e0, tab), v1 = sb * exp_neg_tab(e1, tab);
     o[(long long)k * mc + c] = (col_ok && k < n) ? v0 : 0.0;
     o[(long long)(k + 1) * mc + c] = (col_ok && k + 1 < n) ? v1 : 0.0;
   }
