@@ -280,10 +280,256 @@ extern "C" int gp_rowscale(double* M, int rows, int cols, int ld, const double* 
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }
 
+namespace {
+
+// ---- Tall-skinny products of the randomized SVD (src/svd.py:52-64 at the fit's shapes) ------
+// The four products that stream the ensemble X (n_sims x ny, C-order: ny = 1,347,945 at the
+// fit's 512 runs) against r = p + k <= 32 test vectors read X once each and are HBM-bound
+// (5.5 GB in fp64; their fp64 MFMA time at r padded to 32 is ~0.6 ms, the read ~0.9 ms at
+// 6 TB/s).  The 64 x 64-tile GEMM above reached 0.20-0.35 of HBM on them (r = 25 of 64 tile
+// columns, one K-step of staging in flight: profiles/r04/r04k_prof_pca.log).  Two kernels keep
+// the narrow side in registers / L2 and stream X with many loads in flight:
+//   tsk (C = X W, K = ny long, C small): every block owns one K-slice of all rows (row groups of
+//       kTskRows), each wave 8 row tiles x 2 column tiles of 16 in MFMA accumulators, the X
+//       operand loaded straight into the MFMA A layout one K-group ahead; partial C per slice,
+//       then splitk_reduce_kernel (fixed order: deterministic);
+//   tsm (C = X^T Y or Q^T X, the big side is the output): every block owns kTsmRows rows of the
+//       big dimension and the whole K <= kTsmMaxK, the narrow operand staged once in LDS; the
+//       accumulators go through LDS so the output is written as contiguous runs.
+// The operands' element types are template parameters (float32 X read as stored and widened
+// exactly, as the general kernel does), so float32 and fp64 operands give the same bits.
+constexpr int kTskRows = 512;        // rows of C per tsk block (4 waves x 128)
+constexpr int kTskMinK = 1 << 16;
+constexpr int kTsmRows = 256;        // rows of the big dimension per tsm block (4 waves x 64)
+constexpr int kTsmMaxK = 1024;   // K of a tsm product (the number of runs)
+constexpr int kTsMaxN = 32;          // narrow side (two 16-wide MFMA column tiles)
+
+// K-groups (16 k each) in flight ahead of the one being multiplied (a ring of kTsRing register
+// buffers, indexed at compile time: the loops below are unrolled over the ring)
+constexpr int kTsRing = 3;    // tsm
+constexpr int kTskRing = 2;   // tsk: 8 row tiles per wave, one group ahead (registers)
+
+// C(i, j) = sum_k P(i, k) W(k, j) for i < M (P(i,k) = P[k + i*ldp], contiguous in k), j < N <= 32,
+// W(k, j) = W[k*wk + j*wj], k in this block's slice; partial C to part[slice][j*M + i].
+template <typename EP, typename EW>
+__global__ __launch_bounds__(256, 1) void gemm_tsk_kernel(int M, int N, int K, int kslice,
+                                                          const EP* __restrict__ P, int ldp,
+                                                          const EW* __restrict__ W, long long wk,
+                                                          long long wj, double* __restrict__ part) {
+  const int slice = blockIdx.x, rg = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, ks = lane >> 4;
+  const int kb = slice * kslice, ke = min(K, kb + kslice);
+  const int row0 = rg * kTskRows + w * 128;
+  f64x4 acc[8][2];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t][0] = acc[t][1] = zero4();
+  // the lane's rows (one per row tile); rows >= M read row 0 and are masked to zero
+  const EP* prow[8];
+  bool rok[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int r = row0 + 16 * t + li;
+    rok[t] = r < M;
+    prow[t] = P + (long long)(rok[t] ? r : 0) * ldp;
+  }
+  const int jc0 = li, jc1 = 16 + li;
+  // one K-group = 16 k = 4 MFMA k-steps: lane (row li, slot ks) holds k = k0 + 4u + ks
+  double a[kTskRing][8][4], bv[kTskRing][4][2];
+  auto load = [&](double (&ab)[8][4], double (&bb)[4][2], int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 4 * u + ks;
+      const bool kok = k < ke;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) ab[t][u] = (kok && rok[t]) ? static_cast<double>(prow[t][k]) : 0.0;
+      bb[u][0] = (kok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
+      bb[u][1] = (kok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kTskRing - 1; ++q) load(a[q], bv[q], kb + 16 * q);
+  for (int k0 = kb; k0 < ke; k0 += 16 * kTskRing) {
+#pragma unroll
+    for (int q = 0; q < kTskRing; ++q) {
+      const int kq = k0 + 16 * q;
+      if (kq >= ke) break;
+      const int kn = kq + 16 * (kTskRing - 1);            // the group kTskRing - 1 ahead
+      if (kn < ke) load(a[(q + kTskRing - 1) % kTskRing], bv[(q + kTskRing - 1) % kTskRing], kn);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          acc[t][0] = mfma16x16x4(a[q][t][u], bv[q][u][0], acc[t][0]);
+          acc[t][1] = mfma16x16x4(a[q][t][u], bv[q][u][1], acc[t][1]);
+        }
+    }
+  }
+  // C layout: lane l, reg q holds C[(l >> 4) + 4q][l & 15] of each 16 x 16 tile
+  double* pp = part + (long long)slice * M * N;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = row0 + 16 * t + ks + 4 * q, j = 16 * jt + li;
+        if (r < M && j < N) pp[(long long)j * M + r] = acc[t][jt][q];
+      }
+}
+
+// C(i, j) = alpha sum_k P(i, k) Q(k, j) + beta C(i, j) for i < M (P(i,k) = P[i + k*ldp],
+// contiguous in i), j < N <= 32, k < K <= kTsmMaxK, Q(k, j) = Q[k*qk + j*qj] (read through L1 /
+// L2: 100 KB at the fit's 512 x 25), C(i, j) = C[i*ci + j*cj].  The block's rows are written
+// through LDS as runs along whichever of i / j is contiguous in C.
+template <typename EP, typename EQ>
+__global__ __launch_bounds__(256, 1) void gemm_tsm_kernel(int M, int N, int K,
+                                                          const EP* __restrict__ P, int ldp,
+                                                          const EQ* __restrict__ Q, long long qk,
+                                                          long long qj, double alpha,
+                                                          double beta, double* __restrict__ C,
+                                                          long long ci, long long cj) {
+  __shared__ double cs[kTsmRows * 33];            // the block's C rows, pitch 33
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, ks = lane >> 4;
+  const long long i0 = (long long)blockIdx.x * kTsmRows;
+  f64x4 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = zero4();
+  const long long rbase = i0 + w * 64;
+  const EP* pcol[4];
+  bool rok[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const long long r = rbase + 16 * t + li;
+    rok[t] = r < M;
+    pcol[t] = P + (rok[t] ? r : 0);
+  }
+  const int jc0 = li, jc1 = 16 + li;
+  // K-group of 16: lane (row li, slot ks) holds k = k0 + 4u + ks of its 4 row tiles
+  double a[kTsRing][4][4], bv[kTsRing][4][2];
+  auto load = [&](double (&ab)[4][4], double (&bb)[4][2], int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 4 * u + ks;
+      const bool kok = k < K;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        ab[t][u] = (kok && rok[t]) ? static_cast<double>(pcol[t][(long long)k * ldp]) : 0.0;
+      bb[u][0] = (kok && jc0 < N) ? static_cast<double>(Q[k * qk + jc0 * qj]) : 0.0;
+      bb[u][1] = (kok && jc1 < N) ? static_cast<double>(Q[k * qk + jc1 * qj]) : 0.0;
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kTsRing - 1; ++q) load(a[q], bv[q], 16 * q);
+  for (int k0 = 0; k0 < K; k0 += 16 * kTsRing) {
+#pragma unroll
+    for (int q = 0; q < kTsRing; ++q) {
+      const int kq = k0 + 16 * q;
+      if (kq >= K) break;
+      const int kn = kq + 16 * (kTsRing - 1);
+      if (kn < K) load(a[(q + kTsRing - 1) % kTsRing], bv[(q + kTsRing - 1) % kTsRing], kn);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[t][0] = mfma16x16x4(a[q][t][u], bv[q][u][0], acc[t][0]);
+          acc[t][1] = mfma16x16x4(a[q][t][u], bv[q][u][1], acc[t][1]);
+        }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        cs[(w * 64 + 16 * t + ks + 4 * q) * 33 + 16 * jt + li] = acc[t][jt][q];
+  __syncthreads();
+  const int rows = (int)min((long long)kTsmRows, M - i0);
+  if (cj == 1) {                                // C(i, j) runs along j: rows of N doubles
+    for (int e = threadIdx.x; e < rows * N; e += 256) {
+      const int r = e / N, j = e - r * N;
+      double* c = C + (i0 + r) * ci + j;
+      const double v = alpha * cs[r * 33 + j];
+      *c = (beta == 0.0) ? v : fma(beta, *c, v);
+    }
+  } else {                                      // runs along i: one column at a time
+    for (int e = threadIdx.x; e < rows * N; e += 256) {
+      const int j = e / rows, r = e - j * rows;
+      double* c = C + (i0 + r) * ci + j * cj;
+      const double v = alpha * cs[r * 33 + j];
+      *c = (beta == 0.0) ? v : fma(beta, *c, v);
+    }
+  }
+}
+
+// Which tall-skinny kernel serves (transa, transb, m, n, k), if any:
+//   1 tsk: transa = 1 (A's columns are C's rows), n <= 32, k >= kTskMinK;
+//   2 tsm: transa = 0, n <= 32, k <= kTsmMaxK, m >= 8192 (the big side is C's rows);
+//   3 tsm on the transpose: transb = 1, m <= 32, k <= kTsmMaxK, n >= 8192 (C^T's rows).
+int ts_kind(int transa, int transb, int m, int n, int k) {
+  if (transa == 1 && n <= kTsMaxN && k >= kTskMinK) return 1;
+  if (transa == 0 && n <= kTsMaxN && k <= kTsmMaxK && m >= 8192) return 2;
+  if (transb == 1 && m <= kTsMaxN && k <= kTsmMaxK && n >= 8192) return 3;
+  return 0;
+}
+
+// tsk's K slices: about two blocks per CU over all row groups, each slice a multiple of 16.
+void tsk_shape(int m, int k, int& groups, int& slices, int& kslice) {
+  groups = gp_ceil_div(m, kTskRows);
+  slices = max(1, 512 / groups);
+  kslice = gp_ceil_div(gp_ceil_div(k, slices), 16) * 16;
+  slices = gp_ceil_div(k, kslice);
+}
+
+}  // namespace
+
 extern "C" long long gp_dgemm_ws_bytes(int m, int n, int k) {
   if (m <= 0 || n <= 0 || k <= 0) return 0;
   const int s = choose_splits(m, n, k);
-  return s > 1 ? (long long)s * m * n * 8 : 0;
+  long long bytes = s > 1 ? (long long)s * m * n * 8 : 0;
+  if (n <= kTsMaxN && k >= kTskMinK) {            // a tsk product (transa = 1)
+    int g, sl, kc;
+    tsk_shape(m, k, g, sl, kc);
+    bytes = max(bytes, (long long)sl * m * n * 8);
+  }
+  return bytes;
+}
+
+namespace {
+template <typename EA, typename EB>
+hipError_t launch_ts(int kind, int transa, int transb, int m, int n, int k, double alpha,
+                            const void* A, int lda, const void* B, int ldb, double beta,
+                            double* C, int ldc, double* part, hipStream_t stream) {
+  const EA* a = static_cast<const EA*>(A);
+  const EB* b = static_cast<const EB*>(B);
+  if (kind == 1) {
+    int groups, slices, kslice;
+    tsk_shape(m, k, groups, slices, kslice);
+    // W(k, j) = opB(k, j): transb 0 -> B[k + j*ldb], 1 -> B[j + k*ldb]
+    const long long wk = transb ? ldb : 1, wj = transb ? 1 : ldb;
+    hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(256), 0, stream, m,
+                       n, k, kslice, a, lda, b, wk, wj, part);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const long long tot = (long long)m * n;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       stream, part, slices, m, n, alpha, beta, C, ldc);
+    return hipGetLastError();
+  }
+  if (kind == 2) {
+    // C(i, j) = sum_k A[i + k*lda] opB(k, j), C[i + j*ldc]
+    const long long qk = transb ? ldb : 1, qj = transb ? 1 : ldb;
+    hipLaunchKernelGGL((gemm_tsm_kernel<EA, EB>), dim3(gp_ceil_div(m, kTsmRows)), dim3(256), 0,
+                       stream, m, n, k, a, lda, b, qk, qj, alpha, beta, C, 1LL, (long long)ldc);
+  } else {
+    // C^T(j, i) = sum_k B[j + k*ldb] opA(i, k), C[i + j*ldc]: the big operand is B
+    const long long qk = transa ? 1 : lda, qj = transa ? lda : 1;
+    hipLaunchKernelGGL((gemm_tsm_kernel<EB, EA>), dim3(gp_ceil_div(n, kTsmRows)), dim3(256), 0,
+                       stream, n, m, k, b, ldb, a, qk, qj, alpha, beta, C, (long long)ldc, 1LL);
+  }
+  return hipGetLastError();
 }
 
 template <typename EA, typename EB>
@@ -301,6 +547,8 @@ static void launch_gemm(int transa, int transb, dim3 grid, hipStream_t stream, i
   else GP_GEMM(1, 1);
 #undef GP_GEMM
 }
+
+}  // namespace
 
 extern "C" int gp_gemm_ex(int transa, int transb, int m, int n, int k, double alpha,
                           const void* A, int a_f32, int lda, const void* B, int b_f32, int ldb,
@@ -320,6 +568,32 @@ extern "C" int gp_gemm_ex(int transa, int transb, int m, int n, int k, double al
   if (!C) return -14;
   if (ldc < m || ldc < 1) return -15;
   if (m == 0 || n == 0) return 0;
+  const int tk = (k > 0) ? ts_kind(transa, transb, m, n, k) : 0;
+  if (tk) {
+    long long need = 0;
+    if (tk == 1) {
+      int g, sl, kc;
+      tsk_shape(m, k, g, sl, kc);
+      need = (long long)sl * m * n * 8;
+    }
+    if (tk != 1 || (ws && ws_bytes >= need)) {
+      hipError_t e;
+      double* part = static_cast<double*>(ws);
+      if (a_f32 && b_f32)
+        e = launch_ts<float, float>(tk, transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C,
+                                    ldc, part, stream);
+      else if (a_f32)
+        e = launch_ts<float, double>(tk, transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C,
+                                     ldc, part, stream);
+      else if (b_f32)
+        e = launch_ts<double, float>(tk, transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C,
+                                     ldc, part, stream);
+      else
+        e = launch_ts<double, double>(tk, transa, transb, m, n, k, alpha, A, lda, B, ldb, beta,
+                                      C, ldc, part, stream);
+      return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+    }
+  }
   int splits = (k > 0) ? choose_splits(m, n, k) : 1;
   if (splits > 1 && (!ws || ws_bytes < (long long)splits * m * n * 8)) splits = 1;
   const int kchunk = (k > 0) ? gp_ceil_div(gp_ceil_div(k, splits), TB) * TB : TB;

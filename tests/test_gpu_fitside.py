@@ -23,7 +23,8 @@ def _t(a, dev):
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (70, 33, 129), (128, 64, 64), (17, 5, 60000)])
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (70, 33, 129), (128, 64, 64), (17, 5, 60000),
+                                   (512, 25, 70001), (20001, 25, 300), (25, 20001, 300)])
 def test_gemm(dev, ta, tb, m, n, k):
     from gladsgp_amd.blas import CM, gemm
     rng = np.random.default_rng(m + n + k + ta * 2 + tb)
@@ -41,7 +42,11 @@ def test_gemm(dev, ta, tb, m, n, k):
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("m,n,k", [(70, 33, 129), (512, 25, 40000), (3, 200, 7)])
+@pytest.mark.parametrize("m,n,k", [(70, 33, 129), (512, 25, 40000), (3, 200, 7),
+                                   # the tall-skinny kernels (blas.hip ts_kind): tsk (long K,
+                                   # ta = 1), tsm (K <= 1024, the big side C's rows / C^T's)
+                                   (512, 25, 70001), (700, 7, 65537), (20001, 25, 300),
+                                   (25, 20001, 300), (32, 9000, 512)])
 def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
     """gp_gemm_ex with a float32 A and/or B (widened on load) equals gp_gemm_ex / gp_dgemm on
     fp64 copies of the same values bit for bit, split-K shapes included (512 x 25 x 40000 is
