@@ -447,8 +447,9 @@ int gp_comm_destroy(void* comm);
 int gp_bcast(void* comm, void* buf, long long bytes, int root, hipStream_t stream);
 
 /* Lower triangle of a column-major n x n matrix (leading dimension ld; column c from row c
- * on) to / from a contiguous vector of n (n + 1) / 2 doubles, column after column: the payload
- * of the single-GP L^-1 broadcast (about half the padded square the prediction reads).
+ * on) to / from a contiguous vector of n (n + 1) / 2 doubles, column after column (round 4's
+ * single-GP broadcast payload; the payload is now gp_pack_linv's tile-packed layout, which the
+ * prediction reads in place).
  * gp_unpack_tril writes only the lower triangle (the strict upper part of A is left as it
  * is: zero in a buffer prepared for gp_predict). */
 int gp_pack_tril(const double* A, int n, int ld, double* out, hipStream_t stream);

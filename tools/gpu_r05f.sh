@@ -6,3 +6,11 @@ rc=$?; tail -3 gpurun_out/r05f_pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python tools/prof_pca.py > gpurun_out/r05f_prof_pca.log 2>&1 || exit 1
 grep -E "init_model|gemm\(" gpurun_out/r05f_prof_pca.log | head -20
 timeout -k 10 900 bash tools/ab_bench_libs.sh r05f_ab _ab/libgpfit_pk_new.so _ab/libgpfit_tabexp_ts.so || exit 1
+for rep in 1 2 3; do
+  timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/r05f_ev.log 2>&1 || exit 1
+  GPFIT_BENCH_NOEVENTS=1 timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/r05f_noev.log 2>&1 || exit 1
+  python3 -c "
+import json
+f=lambda p: json.loads([x for x in open(p).read().splitlines() if x.startswith('{')][-1])['ms_per_step']
+print('events %.3f ms  no events %.3f ms' % (f('gpurun_out/r05f_ev.log'), f('gpurun_out/r05f_noev.log')))" | tee -a gpurun_out/r05f_events_ab.log
+done

@@ -19,16 +19,18 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     rows = list(csv.DictReader(open(f[0])))
     agg = collections.defaultdict(list)
     for r in rows:
-        agg[r["Kernel_Name"][:50]].append(float(r["Counter_Value"]))
+        agg[r["Kernel_Name"][:60]].append(float(r["Counter_Value"]))
     for k, v in agg.items():
         print(f"{c:11s} {k:50s} n={len(v):4d} mean={sum(v)/len(v):14.1f} (KB per dispatch)")
-        means[k.replace("(anonymous namespace)::", "").split("(")[0]][c] = sum(v) / len(v)
+        key = k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+        means[key.split("<")[0]][c] = sum(v) / len(v)     # trmm_pair_kernel<false> -> base name
 # the dominant kernel's HBM-side bytes per launch for bench.py's roofline.traffic: FETCH_SIZE x2
 # (gfx950 reports half the bytes of 16-B/lane streams, MI355X_MICROARCH.md HBM section) + WRITE
 t = means.get("trmm_pair_kernel", {})
 if t:
     if WL == "c3":
-        n, m, chunk, batch, launches = 4096, 100000, 16384, 1, 7
+        # 6 launches per step since round 5 (the 1696-point tail runs merged with chunk 6)
+        n, m, chunk, batch, launches = 4096, 100000, 16384, 1, 6
     else:                                # C4: 32 GPs, n = 1024, 8192-point chunks
         n, m, chunk, batch, launches = 1024, 100000, 8192, 32, 13
     L = 8.0 * n * (n + 1) / 2 * batch    # L^-1 lower triangles
