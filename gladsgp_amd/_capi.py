@@ -118,6 +118,7 @@ SIGNATURES = {
     "gp_unpack_tril": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "gp_gather": (c_int, [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_void_p]),
     "gp_profile_enable": (c_int, [c_int]),
+    "gp_profile_select": (ctypes.c_uint, [ctypes.c_uint]),
     "gp_profile_reset": (c_int, []),
     "gp_profile_read": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
     "gp_set_poll_budget": (c_ll, [c_ll]),

@@ -18,12 +18,13 @@ struct Slot {
 };
 
 bool g_enabled = false;
+unsigned g_mask = ~0u;             // kernels that record (gp_profile_select)
 Slot g_slots[GP_PROF_NUM];
 
 }  // namespace
 
 void gpfit_prof_begin_n(int id, hipStream_t st, int launches) {
-  if (!g_enabled || id < 0 || id >= GP_PROF_NUM) return;
+  if (!g_enabled || id < 0 || id >= GP_PROF_NUM || !(g_mask >> id & 1u)) return;
   Slot& s = g_slots[id];
   if (s.used >= (int)s.start.size()) return;   // capacity exhausted: stop recording
   s.launches[s.used] = launches > 0 ? launches : 1;
@@ -33,7 +34,7 @@ void gpfit_prof_begin_n(int id, hipStream_t st, int launches) {
 void gpfit_prof_begin(int id, hipStream_t st) { gpfit_prof_begin_n(id, st, 1); }
 
 void gpfit_prof_end(int id, hipStream_t st) {
-  if (!g_enabled || id < 0 || id >= GP_PROF_NUM) return;
+  if (!g_enabled || id < 0 || id >= GP_PROF_NUM || !(g_mask >> id & 1u)) return;
   Slot& s = g_slots[id];
   if (s.used >= (int)s.start.size()) return;
   (void)hipEventRecord(s.stop[s.used], st);
@@ -60,6 +61,12 @@ extern "C" int gp_profile_enable(int capacity) {
   }
   g_enabled = capacity > 0;
   return 0;
+}
+
+extern "C" unsigned gp_profile_select(unsigned mask) {
+  const unsigned old = g_mask;
+  g_mask = mask;
+  return old;
 }
 
 extern "C" int gp_profile_reset(void) {

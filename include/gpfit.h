@@ -473,6 +473,9 @@ int gp_gather(void* comm, const void* send, long long bytes, void* recv, int roo
 #define GP_PROF_CROSS 3       /* predict: per-chunk cross-covariance build               */
 #define GP_PROF_NUM 4
 int gp_profile_enable(int capacity);
+/* Which kernels record (bit GP_PROF_* set; default all): a timed run can keep only the
+ * dominant kernel's event pair on the critical path.  Returns the previous mask. */
+unsigned gp_profile_select(unsigned mask);
 int gp_profile_reset(void);
 int gp_profile_read(int id, int* count, double* total_ms, double* max_ms);
 

@@ -14,3 +14,4 @@ import json
 f=lambda p: json.loads([x for x in open(p).read().splitlines() if x.startswith('{')][-1])['ms_per_step']
 print('events %.3f ms  no events %.3f ms' % (f('gpurun_out/r05f_ev.log'), f('gpurun_out/r05f_noev.log')))" | tee -a gpurun_out/r05f_events_ab.log
 done
+timeout -k 10 900 bash tools/sweep_c4_aux.sh r05f_c4aux "8192:4 8192:7 8192:13" || exit 1
