@@ -44,6 +44,11 @@ def test_every_declared_symbol_is_exported(lib):
     for name in _declared():
         assert name in exported, name
         assert name in _capi.SIGNATURES, f"{name} lacks a ctypes signature"
+    # _capi.lib() binds what it finds (older builds in same-box A/B runs): the shipped build
+    # must export every signature it knows
+    for name in _capi.SIGNATURES:
+        assert name in exported, name
+        assert getattr(lib, name).argtypes is not None or not _capi.SIGNATURES[name][1], name
 
 
 def test_library_has_gfx950_code_object():
