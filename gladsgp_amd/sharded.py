@@ -271,8 +271,9 @@ def balanced_split(m: int, world: int, t_fact: float, T, granule: int = 128) -> 
 
 def calibrate_split(ctx: gdist.Context, X, Xs, beta, s, delta, s_pred, w, m_chunk: int = 0,
                     reps: int = 3):
-    """Rank 0 measures the factorisation (Gram + gp_potrf_inv) and the prediction time of
-    candidate point counts (kernels.predict on the first points of ``Xs``, median of ``reps``)
+    """Rank 0 measures the factorisation (Gram + gp_potrf_inv + the broadcast payload's pack and
+    z) and the prediction time of candidate point counts (kernels.predict from that payload on
+    the first points of ``Xs``, median of ``reps``)
     and picks the split with :func:`balanced_split`; the counts are broadcast so every rank
     uses the same.  Returns (counts, t_fact, t_point) -- t_point at a full 16384-point chunk,
     for reporting.  One rank: ([m], nan, nan) with nothing measured.  The result is memoised
@@ -292,24 +293,33 @@ def calibrate_split(ctx: gdist.Context, X, Xs, beta, s, delta, s_pred, w, m_chun
         return _SPLIT_CACHE[key]
     buf = torch.zeros(world + 2, dtype=F64, device=dev)
     if ctx is None or not ctx.distributed or ctx.rank == 0:
+        # rank 0's extra work per GP: Gram + factorisation + the payload (tile-packed L^-1 and
+        # z = L^-1 w); every rank's prediction: from the payload with z given (no trmv), as
+        # PipelinedPredictor and predict_sharded(mode="broadcast") run it
+        npad = kernels.padded_n(X.shape[0])
+        packer = LinvPacker(npad, dev, n=X.shape[0])
+        payload = packer.buffer(dev)
         tf = []
         for _ in range(reps):
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             ch = kernels.cholesky_inverse(kernels.gram(X, beta, s, delta))
+            packer.pack(ch.linv_buf, ch.info, payload, w=w)
             torch.cuda.synchronize(dev)
             tf.append(time.perf_counter() - t0)
         t_fact = sorted(tf)[reps // 2]
         ws = kernels.PredictWorkspace()
+        view = packer.view(payload)
 
         def T(points):
             Xc = Xs[:points].contiguous()
-            kernels.predict(ch, X, Xc, beta, s, s_pred, w, m_chunk=m_chunk, workspace=ws)
+            kernels.predict(view, X, Xc, beta, s, s_pred, None, m_chunk=m_chunk, workspace=ws)
             ts = []
             for _ in range(reps):
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-                kernels.predict(ch, X, Xc, beta, s, s_pred, w, m_chunk=m_chunk, workspace=ws)
+                kernels.predict(view, X, Xc, beta, s, s_pred, None, m_chunk=m_chunk,
+                                workspace=ws)
                 torch.cuda.synchronize(dev)
                 ts.append(time.perf_counter() - t0)
             return sorted(ts)[reps // 2]
@@ -351,7 +361,8 @@ class PipelinedPredictor:
     """
 
     def __init__(self, ctx: gdist.Context, X: torch.Tensor, Xs: torch.Tensor, w: torch.Tensor,
-                 counts: list[int] | None = None, calib_gp=None, m_chunk: int = 0):
+                 counts: list[int] | None = None, calib_gp=None, m_chunk: int = 0,
+                 receiver_path: bool = False):
         self.ctx = ctx
         self.dev = X.device
         self.X = X.contiguous()
@@ -359,6 +370,9 @@ class PipelinedPredictor:
         self.m = Xs.shape[0]
         self.w = w.reshape(1, self.n).contiguous()
         self.m_chunk = m_chunk
+        # test hook: rank 0 also predicts from the broadcast payload (tile-packed L^-1 + z in
+        # place), the path every other rank takes -- so a one-rank run exercises it
+        self.receiver_path = receiver_path
         self.dist = ctx is not None and ctx.distributed   # collectives (also at world 1)
         world = ctx.world if self.dist else 1
         self.world, self.rank = world, (ctx.rank if self.dist else 0)
@@ -456,7 +470,8 @@ class PipelinedPredictor:
         # rank 0 predicts from its padded L^-1, every other rank from the payload in place (no
         # unpack); all of them with the shipped z (no trmv)
         ch = (kernels.Cholesky(self.n, None, self.linv[cur], self.info, self.logdet)
-              if self.rank == 0 else self.packer.view(self.packed[cur], self.info))
+              if self.rank == 0 and not self.receiver_path
+              else self.packer.view(self.packed[cur], self.info))
         if self.ml:
             kernels.predict(ch, self.X, self.Xl, b, s, sp, w, m_chunk=self.m_chunk,
                             workspace=self.ws, out=(self.out[0:1, : self.ml],

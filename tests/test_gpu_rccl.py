@@ -116,6 +116,28 @@ def _worker(rank, port, results, tmpdir):
         out["pipe_counts"] = pp.counts
         out["pipe"] = [bool(torch.equal(res[k][0], direct[k][0][0]) and
                             torch.equal(res[k][1], direct[k][1][0])) for k in range(3)]
+        # the ranks >= 1 path forced on the one rank: prediction straight from the broadcast
+        # payload (tile-packed L^-1 read in place, z shipped: no unpack, no trmv launched --
+        # kernels.predict is handed z, so gp_predict_ex skips its trmv)
+        seen = []
+        real_predict = kernels.predict
+
+        def spy(chol, *a, **kw):
+            seen.append((type(chol).__name__, kw.get("z") is not None))
+            return real_predict(chol, *a, **kw)
+
+        kernels.predict = spy
+        try:
+            pr = PipelinedPredictor(ctx, Xd, Xsd, yd, counts=[m], receiver_path=True)
+            pr.start(gps[0])
+            res_r = [pr.step(gps[k + 1] if k + 1 < 3 else None).clone() for k in range(3)]
+            pr.finish()
+        finally:
+            kernels.predict = real_predict
+        out["pipe_receiver"] = [bool(torch.equal(res_r[k][0], direct[k][0][0]) and
+                                     torch.equal(res_r[k][1], direct[k][1][0]))
+                                for k in range(3)]
+        out["receiver_calls"] = seen
         # a failed factorisation raises through the broadcast (rank 0's info travels with it)
         dbad = torch.tensor([-2.0], dtype=torch.float64, device=dev)
         try:
@@ -175,5 +197,7 @@ def test_rccl_world1_every_collective_branch(tmp_path):
     assert all(res["modes"].values()), res["modes"]
     assert res["calib"] and res["pipe_counts"] == [40000], res
     assert all(res["pipe"]), res["pipe"]
+    assert all(res["pipe_receiver"]), res["pipe_receiver"]
+    assert res["receiver_calls"] == [("PackedLinv", True)] * 3, res["receiver_calls"]
     assert res["raised"], res
     assert res["emu_w"] and res["emu_y"] and res["emu_y32"] and res["emu_points"], res
