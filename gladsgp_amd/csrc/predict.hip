@@ -1012,21 +1012,21 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
 
 // ------------------------------------------------------------------------------------------
 // gp_fit_predict: Gram -> Cholesky/L^-1 -> predict as one stream-ordered operation on `stream`.
-// With a context (gp_ctx_create) it forks over the context's three streams (equal priority):
-//   fact: Gram, then the blocked factorisation (latency-bound, few CUs busy);
+// With a context (gp_ctx_create) it forks over the context's two streams (equal priority):
+//   fact: Gram, the blocked factorisation (latency-bound, few CUs busy), then z = L^-1 w and
+//         per chunk, once that chunk's cross-covariance is done, the TRMM (all row tiles of the
+//         chunk, so its K* stays cached), and one mean / var pass over all m points (round 4
+//         ran this on a third stream; the event hop after the factorisation cost 16-20 us);
 //   aux : the cross-covariance of every chunk (independent of the factorisation), CU-masked so
 //         that it leaves aux_free_cus CUs to the factorisation, from the factorisation's
 //         block step cross_start * n/64 on;
-//   pred: once the factorisation is done, z = L^-1 w, then per chunk, once that chunk's
-//         cross-covariance is done, the TRMM (all row tiles of the chunk, so its K* stays
-//         cached), and one mean / var pass over all m points;
 // and joins back into `stream`.  Without a context every step runs in order on `stream`.
 struct gp_ctx_s {
   int device = -1;
   double cross_start = 0.4;
   int aux_chunks = -1;           // cross-covariance chunks on aux (-1: all; gp_ctx_set_aux_chunks)
-  hipStream_t fact = nullptr, aux = nullptr, pred = nullptr;
-  hipEvent_t e_start = nullptr, e_fact = nullptr, e_done = nullptr;
+  hipStream_t fact = nullptr, aux = nullptr;
+  hipEvent_t e_start = nullptr, e_done = nullptr;
   hipEvent_t e_late = nullptr;   // the factorisation has turned latency-bound
   std::vector<hipEvent_t> e_chunk;  // after chunk ch's cross-covariance (grown on demand)
 };
@@ -1052,7 +1052,6 @@ hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
   c->cross_start = cross_start < 0 ? kCrossStart : cross_start;
   const int fr = aux_free_cus < 0 ? kAuxFreeCUs : aux_free_cus;
   if ((e = hipStreamCreateWithFlags(&c->fact, hipStreamNonBlocking)) != hipSuccess) return e;
-  if ((e = hipStreamCreateWithFlags(&c->pred, hipStreamNonBlocking)) != hipSuccess) return e;
   // logical CU i sits on XCD i % 8 (measured with a CU-mask probe in round 1), so masking off
   // the low CUs reserves CUs evenly per XCD
   int ncu = 0;
@@ -1067,7 +1066,7 @@ hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
   } else if ((e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess) {
     return e;
   }
-  hipEvent_t* ev[4] = {&c->e_start, &c->e_fact, &c->e_done, &c->e_late};
+  hipEvent_t* ev[3] = {&c->e_start, &c->e_done, &c->e_late};
   for (hipEvent_t* p : ev)
     if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
   return hipSuccess;
@@ -1079,13 +1078,13 @@ hipError_t ctx_fini(gp_ctx_s* c) {
   int dev0 = 0;
   keep(hipGetDevice(&dev0));
   if (c->device >= 0) keep(hipSetDevice(c->device));
-  hipStream_t st[3] = {c->fact, c->aux, c->pred};
+  hipStream_t st[2] = {c->fact, c->aux};
   for (hipStream_t x : st)
     if (x) {
       keep(hipStreamSynchronize(x));
       keep(hipStreamDestroy(x));
     }
-  hipEvent_t ev[4] = {c->e_start, c->e_fact, c->e_done, c->e_late};
+  hipEvent_t ev[3] = {c->e_start, c->e_done, c->e_late};
   for (hipEvent_t x : ev)
     if (x) keep(hipEventDestroy(x));
   for (hipEvent_t x : c->e_chunk)
@@ -1160,7 +1159,10 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
       S->e_chunk.push_back(ev);
     }
   }
-  hipStream_t fact = S ? S->fact : stream, aux = S ? S->aux : stream, pred = S ? S->pred : stream;
+  // the prediction runs on the factorisation's stream: z and the first TRMM follow the
+  // factorisation without a cross-stream hop (an event wait between pp_kernel and the trmv cost
+  // 16-20 us of every C3 step, profiles/r05/r05a_timeline.txt)
+  hipStream_t fact = S ? S->fact : stream, aux = S ? S->aux : stream, pred = fact;
   if (S) {
     GP_CK(hipEventRecord(S->e_start, stream));
     GP_CK(hipStreamWaitEvent(fact, S->e_start, 0));
@@ -1175,10 +1177,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
                              w.pot, p.bytes - p.off_pot, fact, k_late > 0 ? k_late : -1,
                              (S && k_late > 0) ? S->e_late : nullptr);
   if (rc) return rc;
-  if (S) {
-    GP_CK(hipEventRecord(S->e_fact, fact));
-    GP_CK(hipStreamWaitEvent(aux, S->e_late, 0));
-  }
+  if (S) GP_CK(hipStreamWaitEvent(aux, S->e_late, 0));
   // chunks whose cross-covariance runs on aux, beside the factorisation and the earlier TRMMs
   // (all by default; the rest run on pred just before their TRMM: gp_ctx_set_aux_chunks)
   const int n_aux = (S && S->aux_chunks >= 0 && S->aux_chunks < p.nchunks) ? S->aux_chunks
@@ -1196,10 +1195,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   // pred: z, then TRMM + mean / var chunk by chunk.  One launch per chunk (not one for all):
   // the dispatcher interleaves another stream's kernels between launches, so a concurrent
   // factorisation is not starved behind a 25 ms grid (measured: 14 ms vs 3 ms per potrf).
-  if (S) {
-    if (n_aux > 0) GP_CK(hipEventRecord(S->e_chunk[n_aux - 1], aux));   // after the end event
-    GP_CK(hipStreamWaitEvent(pred, S->e_fact, 0));
-  }
+  if (S && n_aux > 0) GP_CK(hipEventRecord(S->e_chunk[n_aux - 1], aux));   // after the end event
   const LinvRef L{Linv, ldinv, strideInv, false};
   GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, pred));
   GP_CK(solve_all(p, w, L, w.z, p.npad, m, s_pred, mean, var, ldo, batch, pred,
