@@ -1085,7 +1085,9 @@ struct PPArgs {
   long long budget;                   // polls per wait
   int* info; double* logdet;
   const int2* tasks; int ntasks;
-  int* head;                          // [0] dequeue counter, [1] workgroups that have left
+  int groups;                         // 1: one shared queue; 8: per-XCD queues (pp_groups)
+  int* head;                          // [0] dequeue counter, [1] workgroups that have left,
+                                      // [32 + 4g] group g's dequeue counter
   int* flags; int fstride;            // per problem: FL[N*N], FX[N*N], DPF[N], SPF[N], abort
 #ifdef GPFIT_PP_TRACE
   int* dbg;                           // trace build only: per-workgroup progress words
@@ -1768,8 +1770,12 @@ GP_DEV void pp_zero(const PPArgs& P, const PPTask& T) {
 }
 
 __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
+  // per-XCD queues: workgroup w takes group w % 8's tasks, the global tasks 8k + g (pp_groups)
+  const int g = (int)blockIdx.x % P.groups;
   for (;;) {
-    if (threadIdx.x == 0) g_msg[0] = atomicAdd(P.head, 1);
+    if (threadIdx.x == 0)
+      g_msg[0] = P.groups > 1 ? atomicAdd(P.head + 32 + 4 * g, 1) * P.groups + g
+                              : atomicAdd(P.head, 1);
     __syncthreads();
     const int t = g_msg[0];
     __syncthreads();
@@ -1983,6 +1989,10 @@ static int potrf_sweep(double* A, int n, int lda, long long sA, double* X, int l
   return 0;
 }
 
+// gp_set_potrf_path (test / A-B hook): 1 forces the blocked sweep for later factorisations,
+// 2 the persistent kernel with one shared queue for every batch
+static int g_potrf_path = 0;
+
 static int num_cus() {
   static const int ncu = [] {
     int dev = 0, n = 0;
@@ -2023,7 +2033,23 @@ static int pp_lead(int batch, int resident) {
   return (long long)batch * (kPPLeadBlocked + 1) < resident ? kPPLead : 0;
 }
 
-// Scratch of one persistent factorisation: the task list, a 256-B header (dequeue counter, exit
+// Dequeue queues of a batched persistent factorisation.  Every task-list entry of problem b
+// sits at an index congruent to b mod batch (the list is the batch's chains, then each task for
+// b = 0..batch-1 in turn), so for batch % 8 == 0 the entries 8k + g are exactly the tasks of the
+// problems b % 8 == g, in the list's order.  With 8 queues workgroup w dequeues only from queue
+// w % 8: a problem's tasks all run on workgroups w, w + 8, ..., which the dispatcher places on
+// one XCD (round-robin placement, MI355X_MICROARCH.md "Workgroup dispatch"), so the tiles they
+// hand each other and re-read (every L_jk of a row, D_j) are served by that XCD's L2 instead of
+// being fetched once per XCD from the Infinity Fabric.  Placement is a speed assumption only:
+// each queue is a problem-closed, per-problem topological list served by grid / 8 workgroups,
+// and the deadlock argument of pp_schedule_kernel holds per queue (pp_lead / pp_eligible scaled
+// by 8 are the same inequalities).  Not for batch 1 (C3): one problem on one XCD would leave
+// seven idle.
+static int pp_groups(int batch, int grid) {
+  return (g_potrf_path != 2 && batch >= 8 && batch % 8 == 0 && grid % 8 == 0) ? 8 : 1;
+}
+
+// Scratch of one persistent factorisation: the task list, a 256-B header (dequeue counters, exit
 // counter) and the per-problem flag words.
 struct PPScratch {
   long long ntasks;
@@ -2047,12 +2073,10 @@ static bool pp_shape_ok(int n, int batch) {
   return N <= kPPMaxN && pp_task_count(N, true) * (long long)batch < (1ll << 30);
 }
 
-// gp_set_potrf_path (test / A-B hook): 1 forces the blocked sweep for later factorisations
-static int g_potrf_path = 0;
 
 static bool pp_eligible(int n, int batch, int resident) {
   // the chains hold `batch` workgroups for the whole launch: at least as many workers again
-  return g_potrf_path == 0 && pp_shape_ok(n, batch) && 2 * batch <= resident;
+  return g_potrf_path != 1 && pp_shape_ok(n, batch) && 2 * batch <= resident;
 }
 
 // The persistent dataflow factorisation (pp_kernel) on `stream` in the caller's scratch `scr`
@@ -2086,6 +2110,7 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   P.budget = budget > 0 ? budget : kPollBudget;
   P.info = info; P.logdet = logdet;
   P.tasks = tasks; P.ntasks = (int)s.ntasks;
+  P.groups = pp_groups(batch, grid);
   P.head = head; P.flags = flags; P.fstride = s.fstride;
 #ifdef GPFIT_PP_TRACE
   P.dbg = g_trace_dbg;
@@ -2298,10 +2323,11 @@ extern "C" long long gp_set_poll_budget(long long polls) {
 }
 
 // Factorisation path for later enqueues (process-wide test / A-B hook): 0 = automatic (the
-// persistent kernel where eligible), 1 = always the blocked sweep.  Returns the previous value.
+// persistent kernel where eligible, per-XCD queues for batches of 8k), 1 = always the blocked
+// sweep, 2 = the persistent kernel with one shared queue.  Returns the previous value.
 extern "C" int gp_set_potrf_path(int path) {
   const int prev = g_potrf_path;
-  g_potrf_path = path == 1 ? 1 : 0;
+  g_potrf_path = (path == 1 || path == 2) ? path : 0;
   return prev;
 }
 

@@ -490,8 +490,9 @@ long long gp_set_poll_budget(long long polls);
 
 /* Test / A-B hook, process-wide: the factorisation path of gp_potrf_inv / gp_potrf /
  * gp_fit_predict / gp_loglik enqueued afterwards.  0 = automatic (the persistent dataflow
- * kernel where eligible, else the blocked sweep), 1 = always the blocked right-looking sweep.
- * Returns the previous setting. */
+ * kernel where eligible -- with per-XCD task queues for batches that are multiples of 8 --,
+ * else the blocked sweep), 1 = always the blocked right-looking sweep, 2 = the persistent
+ * kernel with one shared task queue for every batch.  Returns the previous setting. */
 int gp_set_potrf_path(int path);
 
 #ifdef __cplusplus

@@ -145,3 +145,35 @@ def test_sweep_multi_tile_matches_persistent(dev):
     La, Lb = a.L.cpu().numpy(), b.L.cpu().numpy()
     for k in range(B):
         assert np.max(np.abs(La[k] - Lb[k])) <= 1e-11 * np.max(np.abs(La[k]))
+
+
+@pytest.mark.parametrize("n,B", [(512, 24), (1024, 32), (1000, 16)])
+def test_xcd_queues_match_shared_queue(dev, n, B):
+    """Batches of 8k run the persistent factorisation from per-XCD task queues
+    (gp_set_potrf_path(0)); every tile keeps its K order, so L, L^-1 and logdet are bit-identical
+    to the one-shared-queue launch (path 2).  A non-PD problem aborts only itself (info at its
+    failing column), whichever queue it sits in."""
+    from gladsgp_amd import _capi, kernels
+    rng = np.random.default_rng(23)
+    X = rng.random((n, 8))
+    betas = rng.uniform(0.5, 5, (B, 8))
+    G = kernels.gram(_t(X, dev), _t(betas, dev), 1.0, 1e-5)
+    bad = 8 + 3                                      # queue 3 of the per-XCD launch
+    G[bad, 700 % n, 700 % n] = -1.0
+    a = kernels.cholesky_inverse(G.clone())
+    prev = _capi.lib().gp_set_potrf_path(2)
+    try:
+        b = kernels.cholesky_inverse(G.clone())
+        torch.cuda.synchronize()
+    finally:
+        assert _capi.lib().gp_set_potrf_path(prev) == 2
+    ia, ib = a.info.cpu().tolist(), b.info.cpu().tolist()
+    assert ia == ib
+    assert ia[bad] > 0 and [v for k, v in enumerate(ia) if k != bad] == [0] * (B - 1)
+    ok = [k for k in range(B) if k != bad]
+    assert torch.equal(a.L[ok], b.L[ok])
+    assert torch.equal(a.Linv[ok], b.Linv[ok])
+    assert torch.equal(a.logdet[ok], b.logdet[ok])
+    Gb = gp_ref.gram_ardse(X, betas[0], 1.0, 1e-5)
+    L = a.L[0].cpu().numpy()
+    assert np.linalg.norm(L @ L.T - Gb) / np.linalg.norm(Gb) <= 1e-13

@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 : > gpurun_out/$TAG.log
 for cfg in $CFGS $REV; do
   ch=${cfg%%:*}; ax=${cfg#*:}
-  timeout -k 10 200 python bench.py --workload c4 --steps 5 --warmup 2 --m-chunk $ch --aux-chunks $ax > gpurun_out/${TAG}_one.log 2>&1 || { cat gpurun_out/${TAG}_one.log; exit 1; }
+  timeout -k 10 200 python bench.py --workload c4 --steps 5 --warmup 2 --m-chunk $ch --aux-chunks $ax --no-cpu > gpurun_out/${TAG}_one.log 2>&1 || { cat gpurun_out/${TAG}_one.log; exit 1; }
   python -c "
 import json
 l=json.loads([x for x in open('gpurun_out/${TAG}_one.log').read().splitlines() if x.startswith('{')][-1])
