@@ -153,6 +153,9 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
 #define TRMM_XCD_PANELS 8
 #endif
 constexpr int kXcdPanels = TRMM_XCD_PANELS;
+#ifndef TRMM_PAIR_MIX
+#define TRMM_PAIR_MIX 0
+#endif
 
 // The tile-packed L^-1 (GPFIT_LINV_PACKED, the single-GP broadcast's payload): column k of the
 // padded npad x npad L^-1 from row 16 floor(k / 16) on, columns one after another, so every
@@ -221,6 +224,9 @@ GP_DEV void trmm_block_tiles(int bid, const TrmmArgs& a, int& g, int& I0, int& I
       const int x = bid & 7, t = bid >> 3, per = kXcdPanels * NP;
       const int grp = t / per, j = t - grp * per;
       p = j / kXcdPanels;
+      // pair-order mixes (A/B builds only; every map is a bijection on (p, panel))
+      if (TRMM_PAIR_MIX == 1 && (grp & 1)) p = NP - 1 - p;
+      if (TRMM_PAIR_MIX == 2 && (j & 1)) p = NP - 1 - p;
       g = x + 8 * (grp * kXcdPanels + j % kXcdPanels);
     } else {
       const int r = bid - a.Gx * NP, Gr = a.Gp - a.Gx;
