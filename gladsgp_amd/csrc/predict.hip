@@ -235,6 +235,8 @@ GP_DEV void trmm_block_tiles(int bid, const TrmmArgs& a, int& g, int& I0, int& I
     }
     I0 = a.NI - 1 - p;
     I1 = (I0 == p) ? -1 : p;
+    // (A/B build) the pair's diagonal-first tile first in every other block
+    if (TRMM_PAIR_MIX == 3 && I1 >= 0 && (bid & 8)) { I1 = I0; I0 = p; }
   } else {
     const int t = bid - nA;
     const int q = t / a.Qc;
@@ -322,6 +324,8 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
         double* cur = smem + (s & 1) * STAGE;
         if (s + 1 < BI / BK) issue(L, s_diag + s + 1, smem + ((s + 1) & 1) * STAGE);
         else if (nst > BI / BK) issue(L, 0, smem + ((s + 1) & 1) * STAGE);
+        else if (pass + 1 < npass)               // (a diagonal-only first tile) next tile's
+          issue(Lb + Isecond * BI, first_step(Isecond), smem);   // first stage
         if (s <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, s);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -329,6 +333,8 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
       for (int s = BI / BK; s < nsteps; ++s) {
         double* cur = smem + (s & 1) * STAGE;
         if (s + 1 < nst) issue(L, s + 1 - BI / BK, smem + ((s + 1) & 1) * STAGE);
+        else if (pass + 1 < npass)               // next tile's first stage
+          issue(Lb + Isecond * BI, first_step(Isecond), smem);
         trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
