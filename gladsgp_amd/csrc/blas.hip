@@ -289,86 +289,99 @@ namespace {
 // 6 TB/s).  The 64 x 64-tile GEMM above reached 0.20-0.35 of HBM on them (r = 25 of 64 tile
 // columns, one K-step of staging in flight: profiles/r04/r04k_prof_pca.log).  Two kernels keep
 // the narrow side in registers / L2 and stream X with many loads in flight:
-//   tsk (C = X W, K = ny long, C small): every block owns one K-slice of all rows (row groups of
-//       kTskRows), each wave 8 row tiles x 2 column tiles of 16 in MFMA accumulators, the X
-//       operand loaded straight into the MFMA A layout one K-group ahead; partial C per slice,
-//       then splitk_reduce_kernel (fixed order: deterministic);
+//   tsk (C = X W, K = ny long, C small): every block owns one K-slice of kTskRows rows, each
+//       wave 64 rows (4 row tiles x 2 column tiles of 16 in MFMA accumulators).  X is loaded
+//       row-contiguous (8 lanes read 8 consecutive k of one row: 64 B per row, 8 rows per
+//       load), three K-groups ahead in registers, and transposed into the MFMA A layout through
+//       a wave-private LDS tile; partial C per slice, then splitk_reduce_kernel (fixed order:
+//       deterministic).  (Round 5's first tsk loaded X straight into the A layout -- 16 rows x
+//       32 B per load -- and reached 0.19-0.25 of HBM: profiles/r05/r05g_prof_pca.log.)
 //   tsm (C = X^T Y or Q^T X, the big side is the output): every block owns kTsmRows rows of the
-//       big dimension and the whole K <= kTsmMaxK, the narrow operand staged once in LDS; the
-//       accumulators go through LDS so the output is written as contiguous runs.
+//       big dimension and the whole K <= kTsmMaxK (the narrow operand read through L1 / L2),
+//       three blocks per CU; the accumulators go through LDS so the output is written as
+//       contiguous runs.  (256-row blocks at one per CU reached 0.45 of HBM, r05g_prof_pca.log.)
 // The operands' element types are template parameters (float32 X read as stored and widened
 // exactly, as the general kernel does), so float32 and fp64 operands give the same bits.
-constexpr int kTskRows = 512;        // rows of C per tsk block (4 waves x 128)
+constexpr int kTskRows = 256;        // rows of C per tsk block (4 waves x 64)
 constexpr int kTskMinK = 1 << 16;
-constexpr int kTsmRows = 256;        // rows of the big dimension per tsm block (4 waves x 64)
+constexpr int kTsmRows = 128;        // rows of the big dimension per tsm block (4 waves x 32)
 constexpr int kTsmMaxK = 1024;   // K of a tsm product (the number of runs)
 constexpr int kTsMaxN = 32;          // narrow side (two 16-wide MFMA column tiles)
 
 // K-groups (16 k each) in flight ahead of the one being multiplied (a ring of kTsRing register
 // buffers, indexed at compile time: the loops below are unrolled over the ring)
 constexpr int kTsRing = 3;    // tsm
-constexpr int kTskRing = 2;   // tsk: 8 row tiles per wave, one group ahead (registers)
+constexpr int kTskKG = 8;     // tsk: k per group (8 lanes read 64 contiguous bytes of a row)
+constexpr int kTskRing = 4;   // tsk: groups in registers, three in flight ahead
+constexpr int kTskPitch = 72; // tsk LDS transpose: doubles per k row of a wave's 64-row tile
 
 // C(i, j) = sum_k P(i, k) W(k, j) for i < M (P(i,k) = P[k + i*ldp], contiguous in k), j < N <= 32,
 // W(k, j) = W[k*wk + j*wj], k in this block's slice; partial C to part[slice][j*M + i].
 template <typename EP, typename EW>
-__global__ __launch_bounds__(256, 1) void gemm_tsk_kernel(int M, int N, int K, int kslice,
+__global__ __launch_bounds__(256, 2) void gemm_tsk_kernel(int M, int N, int K, int kslice,
                                                           const EP* __restrict__ P, int ldp,
                                                           const EW* __restrict__ W, long long wk,
                                                           long long wj, double* __restrict__ part) {
+  constexpr int G = kTskKG, R = kTskRing, NQ = 64 * G / 64;   // NQ loads of one group per lane
+  __shared__ double xs[4 * G * kTskPitch];
   const int slice = blockIdx.x, rg = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 15, ks = lane >> 4;
+  const int kk = lane % G, rr = lane / G;                // load slot: k offset, row offset
   const int kb = slice * kslice, ke = min(K, kb + kslice);
-  const int row0 = rg * kTskRows + w * 128;
-  f64x4 acc[8][2];
+  const int row0 = rg * kTskRows + w * 64;
+  double* xw = xs + w * G * kTskPitch;
+  f64x4 acc[4][2];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) acc[t][0] = acc[t][1] = zero4();
-  // the lane's rows (one per row tile); rows >= M read row 0 and are masked to zero
-  const EP* prow[8];
-  bool rok[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int r = row0 + 16 * t + li;
-    rok[t] = r < M;
-    prow[t] = P + (long long)(rok[t] ? r : 0) * ldp;
-  }
+  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = zero4();
+  // load q of a group: row row0 + (64 / G) q + rr, k = k0 + kk; rows >= M masked (never read)
+  constexpr int RS = 64 / G;
+  const EP* lrow = P + (long long)(row0 + rr) * ldp + kk;
+  const long long qstep = (long long)RS * ldp;
   const int jc0 = li, jc1 = 16 + li;
-  // one K-group = 16 k = 4 MFMA k-steps: lane (row li, slot ks) holds k = k0 + 4u + ks
-  double a[kTskRing][8][4], bv[kTskRing][4][2];
-  auto load = [&](double (&ab)[8][4], double (&bb)[4][2], int k0) {
+  double xr[R][NQ], bv[R][G / 4][2];
+  auto load = [&](double (&xb)[NQ], double (&bb)[G / 4][2], int k0) {
+    const bool kok = k0 + kk < ke;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int q = 0; q < NQ; ++q)
+      xb[q] = (kok && row0 + RS * q + rr < M) ? static_cast<double>(lrow[q * qstep + k0]) : 0.0;
+#pragma unroll
+    for (int u = 0; u < G / 4; ++u) {
       const int k = k0 + 4 * u + ks;
-      const bool kok = k < ke;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) ab[t][u] = (kok && rok[t]) ? static_cast<double>(prow[t][k]) : 0.0;
-      bb[u][0] = (kok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
-      bb[u][1] = (kok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
+      const bool ok = k < ke;
+      bb[u][0] = (ok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
+      bb[u][1] = (ok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
     }
   };
 #pragma unroll
-  for (int q = 0; q < kTskRing - 1; ++q) load(a[q], bv[q], kb + 16 * q);
-  for (int k0 = kb; k0 < ke; k0 += 16 * kTskRing) {
+  for (int q = 0; q < R - 1; ++q) load(xr[q], bv[q], kb + G * q);
+  for (int k0 = kb; k0 < ke; k0 += G * R) {
 #pragma unroll
-    for (int q = 0; q < kTskRing; ++q) {
-      const int kq = k0 + 16 * q;
+    for (int q = 0; q < R; ++q) {
+      const int kq = k0 + G * q;
       if (kq >= ke) break;
-      const int kn = kq + 16 * (kTskRing - 1);            // the group kTskRing - 1 ahead
-      if (kn < ke) load(a[(q + kTskRing - 1) % kTskRing], bv[(q + kTskRing - 1) % kTskRing], kn);
+      const int kn = kq + G * (R - 1);                    // the group R - 1 ahead
+      if (kn < ke) load(xr[(q + R - 1) % R], bv[(q + R - 1) % R], kn);
+      // transpose: xw[k][row] (one wave's LDS: its own DS instructions run in order)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int i = 0; i < NQ; ++i) xw[kk * kTskPitch + RS * i + rr] = xr[q][i];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          acc[t][0] = mfma16x16x4(a[q][t][u], bv[q][u][0], acc[t][0]);
-          acc[t][1] = mfma16x16x4(a[q][t][u], bv[q][u][1], acc[t][1]);
+      for (int u = 0; u < G / 4; ++u) {
+        double a[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) a[t] = xw[(4 * u + ks) * kTskPitch + 16 * t + li];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[t][0] = mfma16x16x4(a[t], bv[q][u][0], acc[t][0]);
+          acc[t][1] = mfma16x16x4(a[t], bv[q][u][1], acc[t][1]);
         }
+      }
     }
   }
   // C layout: lane l, reg q holds C[(l >> 4) + 4q][l & 15] of each 16 x 16 tile
   double* pp = part + (long long)slice * M * N;
 #pragma unroll
-  for (int t = 0; t < 8; ++t)
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -383,7 +396,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tsk_kernel(int M, int N, int K, i
 // L2: 100 KB at the fit's 512 x 25), C(i, j) = C[i*ci + j*cj].  The block's rows are written
 // through LDS as runs along whichever of i / j is contiguous in C.
 template <typename EP, typename EQ>
-__global__ __launch_bounds__(256, 1) void gemm_tsm_kernel(int M, int N, int K,
+__global__ __launch_bounds__(256, 3) void gemm_tsm_kernel(int M, int N, int K,
                                                           const EP* __restrict__ P, int ldp,
                                                           const EQ* __restrict__ Q, long long qk,
                                                           long long qj, double alpha,
@@ -393,28 +406,29 @@ __global__ __launch_bounds__(256, 1) void gemm_tsm_kernel(int M, int N, int K,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 15, ks = lane >> 4;
   const long long i0 = (long long)blockIdx.x * kTsmRows;
-  f64x4 acc[4][2];
+  constexpr int T = kTsmRows / 64;                // row tiles of 16 per wave
+  f64x4 acc[T][2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = zero4();
-  const long long rbase = i0 + w * 64;
-  const EP* pcol[4];
-  bool rok[4];
+  for (int t = 0; t < T; ++t) acc[t][0] = acc[t][1] = zero4();
+  const long long rbase = i0 + w * 16 * T;
+  const EP* pcol[T];
+  bool rok[T];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < T; ++t) {
     const long long r = rbase + 16 * t + li;
     rok[t] = r < M;
     pcol[t] = P + (rok[t] ? r : 0);
   }
   const int jc0 = li, jc1 = 16 + li;
   // K-group of 16: lane (row li, slot ks) holds k = k0 + 4u + ks of its 4 row tiles
-  double a[kTsRing][4][4], bv[kTsRing][4][2];
-  auto load = [&](double (&ab)[4][4], double (&bb)[4][2], int k0) {
+  double a[kTsRing][T][4], bv[kTsRing][4][2];
+  auto load = [&](double (&ab)[T][4], double (&bb)[4][2], int k0) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int k = k0 + 4 * u + ks;
       const bool kok = k < K;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < T; ++t)
         ab[t][u] = (kok && rok[t]) ? static_cast<double>(pcol[t][(long long)k * ldp]) : 0.0;
       bb[u][0] = (kok && jc0 < N) ? static_cast<double>(Q[k * qk + jc0 * qj]) : 0.0;
       bb[u][1] = (kok && jc1 < N) ? static_cast<double>(Q[k * qk + jc1 * qj]) : 0.0;
@@ -432,19 +446,19 @@ __global__ __launch_bounds__(256, 1) void gemm_tsm_kernel(int M, int N, int K,
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < T; ++t) {
           acc[t][0] = mfma16x16x4(a[q][t][u], bv[q][u][0], acc[t][0]);
           acc[t][1] = mfma16x16x4(a[q][t][u], bv[q][u][1], acc[t][1]);
         }
     }
   }
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < T; ++t)
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        cs[(w * 64 + 16 * t + ks + 4 * q) * 33 + 16 * jt + li] = acc[t][jt][q];
+        cs[(w * 16 * T + 16 * t + ks + 4 * q) * 33 + 16 * jt + li] = acc[t][jt][q];
   __syncthreads();
   const int rows = (int)min((long long)kTsmRows, M - i0);
   if (cj == 1) {                                // C(i, j) runs along j: rows of N doubles
