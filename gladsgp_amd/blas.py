@@ -35,7 +35,12 @@ class CM:
 
     @staticmethod
     def of_rowmajor(a: torch.Tensor) -> "CM":
-        """A C-order (r x c) tensor seen column-major is its transpose: (c x r), ld = c."""
+        """A C-order (r x c) tensor seen column-major is its transpose: (c x r), ld = c -- or,
+        for a row-strided view (unit column stride, row stride >= c: the ensemble's padded
+        y_std), ld = its row stride, without a copy."""
+        if a.dim() == 2 and a.shape[0] > 1 and a.shape[1] > 0 and a.stride(1) == 1 and \
+                a.stride(0) >= a.shape[1]:
+            return CM(a, a.shape[1], a.shape[0], a.stride(0))
         a = a.contiguous()
         r, c = a.shape
         return CM(a, c, r, c)

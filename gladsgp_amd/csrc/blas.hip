@@ -478,6 +478,187 @@ __global__ __launch_bounds__(256, 3) void gemm_tsm_kernel(int M, int N, int K,
   }
 }
 
+// ---- 16-byte forms for fp64 operands whose rows / columns start 16-B aligned (the fit's
+// ensemble: y_std is allocated with a padded row stride, emulator.py standardize_y) ------------
+// tsk16: as gemm_tsk_kernel, but 8 lanes read one row's 16 k as 16-B pairs (128 B per row, 8 rows
+// per load; 64 B with 8-B loads); X three groups ahead, W two (a 6-group unrolled ring).
+constexpr int kTsk16Pitch = 68;
+
+template <typename EW>
+__global__ __launch_bounds__(256, 2) void gemm_tsk16_kernel(int M, int N, int K, int kslice,
+                                                            const double* __restrict__ P, int ldp,
+                                                            const EW* __restrict__ W, long long wk,
+                                                            long long wj,
+                                                            double* __restrict__ part) {
+  constexpr int G = 16, RX = 3, RW = 2;
+  __shared__ double xs[4 * G * kTsk16Pitch];
+  const int slice = blockIdx.x, rg = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, ks = lane >> 4;
+  const int c = lane & 7, rr = lane >> 3;                // load slot: k pair 2c, row offset rr
+  const int kb = slice * kslice, ke = min(K, kb + kslice);
+  const int row0 = rg * kTskRows + w * 64;
+  double* xw = xs + w * G * kTsk16Pitch;
+  f64x4 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = zero4();
+  const double* lrow = P + (long long)(row0 + rr) * ldp + 2 * c;
+  const long long qstep = 8LL * ldp;
+  const int jc0 = li, jc1 = 16 + li;
+  double2 xr[RX][8];
+  double bv[RW][4][2];
+  // (k0 + 2c even < ke: the pair's second element is inside the padded row; zeroed past ke)
+  auto load_x = [&](double2 (&xb)[8], int k0) {
+    const int k = k0 + 2 * c;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      double2 v = make_double2(0.0, 0.0);
+      if (k < ke && row0 + 8 * q + rr < M)
+        v = *reinterpret_cast<const double2*>(lrow + q * qstep + k0);
+      if (k + 1 >= ke) v.y = 0.0;
+      xb[q] = v;
+    }
+  };
+  auto load_w = [&](double (&bb)[4][2], int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 4 * u + ks;
+      const bool ok = k < ke;
+      bb[u][0] = (ok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
+      bb[u][1] = (ok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
+    }
+  };
+  load_x(xr[0], kb);
+  load_w(bv[0], kb);
+  load_x(xr[1], kb + G);
+  for (int k0 = kb; k0 < ke; k0 += G * RX * RW) {
+    static_for<0, RX * RW, 1>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      const int kq = k0 + G * q;
+      if (kq >= ke) return;
+      if (kq + 2 * G < ke) load_x(xr[(q + 2) % RX], kq + 2 * G);
+      if (kq + G < ke) load_w(bv[(q + 1) % RW], kq + G);
+      // transpose: xw[k][row] (one wave's LDS: its own DS instructions run in order)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xw[(2 * c) * kTsk16Pitch + 8 * i + rr] = xr[q % RX][i].x;
+        xw[(2 * c + 1) * kTsk16Pitch + 8 * i + rr] = xr[q % RX][i].y;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        double a[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) a[t] = xw[(4 * u + ks) * kTsk16Pitch + 16 * t + li];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[t][0] = mfma16x16x4(a[t], bv[q % RW][u][0], acc[t][0]);
+          acc[t][1] = mfma16x16x4(a[t], bv[q % RW][u][1], acc[t][1]);
+        }
+      }
+    });
+  }
+  double* pp = part + (long long)slice * M * N;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = row0 + 16 * t + ks + 4 * q, j = 16 * jt + li;
+        if (r < M && j < N) pp[(long long)j * M + r] = acc[t][jt][q];
+      }
+}
+
+// tsm16: as gemm_tsm_kernel (128-row blocks, 32 rows per wave), but each lane reads rows
+// (2 li, 2 li + 1) of a column as one 16-B pair: MFMA tile e takes row 2 li + e (256 B per column
+// per load instead of 128).
+template <typename EQ>
+__global__ __launch_bounds__(256, 2) void gemm_tsm16_kernel(int M, int N, int K,
+                                                            const double* __restrict__ P, int ldp,
+                                                            const EQ* __restrict__ Q, long long qk,
+                                                            long long qj, double alpha,
+                                                            double beta, double* __restrict__ C,
+                                                            long long ci, long long cj) {
+  static_assert(kTsmRows == 128, "tsm16: 32 rows per wave");
+  __shared__ double cs[kTsmRows * 33];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, ks = lane >> 4;
+  const long long i0 = (long long)blockIdx.x * kTsmRows;
+  f64x4 acc[2][2];
+  acc[0][0] = acc[0][1] = acc[1][0] = acc[1][1] = zero4();
+  const long long r0 = i0 + w * 32 + 2 * li;             // rows r0, r0 + 1 (even: aligned pair)
+  const bool ok0 = r0 < M, ok1 = r0 + 1 < M;
+  const double* pcol = P + (ok0 ? r0 : 0);
+  const int jc0 = li, jc1 = 16 + li;
+  double2 a[kTsRing][4];
+  double bv[kTsRing][4][2];
+  auto load = [&](double2 (&ab)[4], double (&bb)[4][2], int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 4 * u + ks;
+      const bool kok = k < K;
+      double2 v = make_double2(0.0, 0.0);
+      if (kok && ok0) v = *reinterpret_cast<const double2*>(pcol + (long long)k * ldp);
+      if (!ok1) v.y = 0.0;
+      ab[u] = v;
+      bb[u][0] = (kok && jc0 < N) ? static_cast<double>(Q[k * qk + jc0 * qj]) : 0.0;
+      bb[u][1] = (kok && jc1 < N) ? static_cast<double>(Q[k * qk + jc1 * qj]) : 0.0;
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kTsRing - 1; ++q) load(a[q], bv[q], 16 * q);
+  for (int k0 = 0; k0 < K; k0 += 16 * kTsRing) {
+    static_for<0, kTsRing, 1>([&](auto QQ) {
+      constexpr int q = decltype(QQ)::value;
+      const int kq = k0 + 16 * q;
+      if (kq >= K) return;
+      const int kn = kq + 16 * (kTsRing - 1);
+      if (kn < K) load(a[(q + kTsRing - 1) % kTsRing], bv[(q + kTsRing - 1) % kTsRing], kn);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[0][0] = mfma16x16x4(a[q][u].x, bv[q][u][0], acc[0][0]);
+        acc[0][1] = mfma16x16x4(a[q][u].x, bv[q][u][1], acc[0][1]);
+        acc[1][0] = mfma16x16x4(a[q][u].y, bv[q][u][0], acc[1][0]);
+        acc[1][1] = mfma16x16x4(a[q][u].y, bv[q][u][1], acc[1][1]);
+      }
+    });
+  }
+  // tile e, MFMA row v = ks + 4q is block row w*32 + 2v + e
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        cs[(w * 32 + 2 * (ks + 4 * q) + e) * 33 + 16 * jt + li] = acc[e][jt][q];
+  __syncthreads();
+  const int rows = (int)min((long long)kTsmRows, M - i0);
+  if (cj == 1) {
+    for (int e = threadIdx.x; e < rows * N; e += 256) {
+      const int r = e / N, j = e - r * N;
+      double* cp = C + (i0 + r) * ci + j;
+      const double v = alpha * cs[r * 33 + j];
+      *cp = (beta == 0.0) ? v : fma(beta, *cp, v);
+    }
+  } else {
+    for (int e = threadIdx.x; e < rows * N; e += 256) {
+      const int j = e / rows, r = e - j * rows;
+      double* cp = C + (i0 + r) * ci + j * cj;
+      const double v = alpha * cs[r * 33 + j];
+      *cp = (beta == 0.0) ? v : fma(beta, *cp, v);
+    }
+  }
+}
+
+// 16-B forms apply to an fp64 big operand with 16-B aligned base and an even leading dimension
+// (and, for tsm16, padded columns: a pair never reads past the allocation -- an even ldp >= M
+// rounds M up inside it)
+template <typename E>
+bool ts_vec_ok(const E* p, int ld, int len) {
+  return sizeof(E) == 8 && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && (ld & 1) == 0 &&
+         ld >= ((len + 1) & ~1);
+}
+
 // Which tall-skinny kernel serves (transa, transb, m, n, k), if any:
 //   1 tsk: transa = 1 (A's columns are C's rows), n <= 32, k >= kTskMinK;
 //   2 tsm: transa = 0, n <= 32, k <= kTsmMaxK, m >= 8192 (the big side is C's rows);
@@ -523,8 +704,18 @@ hipError_t launch_ts(int kind, int transa, int transb, int m, int n, int k, doub
     tsk_shape(m, k, groups, slices, kslice);
     // W(k, j) = opB(k, j): transb 0 -> B[k + j*ldb], 1 -> B[j + k*ldb]
     const long long wk = transb ? ldb : 1, wj = transb ? 1 : ldb;
-    hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(256), 0, stream, m,
-                       n, k, kslice, a, lda, b, wk, wj, part);
+    if constexpr (sizeof(EA) == 8) {
+      if (ts_vec_ok(a, lda, k))
+        hipLaunchKernelGGL((gemm_tsk16_kernel<EB>), dim3(slices, groups), dim3(256), 0, stream,
+                           m, n, k, kslice, reinterpret_cast<const double*>(a), lda, b, wk, wj,
+                           part);
+      else
+        hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(256), 0, stream,
+                           m, n, k, kslice, a, lda, b, wk, wj, part);
+    } else {
+      hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(256), 0, stream, m,
+                         n, k, kslice, a, lda, b, wk, wj, part);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const long long tot = (long long)m * n;
@@ -535,11 +726,27 @@ hipError_t launch_ts(int kind, int transa, int transb, int m, int n, int k, doub
   if (kind == 2) {
     // C(i, j) = sum_k A[i + k*lda] opB(k, j), C[i + j*ldc]
     const long long qk = transb ? ldb : 1, qj = transb ? 1 : ldb;
+    if constexpr (sizeof(EA) == 8) {
+      if (ts_vec_ok(a, lda, m)) {
+        hipLaunchKernelGGL((gemm_tsm16_kernel<EB>), dim3(gp_ceil_div(m, kTsmRows)), dim3(256), 0,
+                           stream, m, n, k, reinterpret_cast<const double*>(a), lda, b, qk, qj,
+                           alpha, beta, C, 1LL, (long long)ldc);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((gemm_tsm_kernel<EA, EB>), dim3(gp_ceil_div(m, kTsmRows)), dim3(256), 0,
                        stream, m, n, k, a, lda, b, qk, qj, alpha, beta, C, 1LL, (long long)ldc);
   } else {
     // C^T(j, i) = sum_k B[j + k*ldb] opA(i, k), C[i + j*ldc]: the big operand is B
     const long long qk = transa ? 1 : lda, qj = transa ? lda : 1;
+    if constexpr (sizeof(EB) == 8) {
+      if (ts_vec_ok(b, ldb, n)) {
+        hipLaunchKernelGGL((gemm_tsm16_kernel<EA>), dim3(gp_ceil_div(n, kTsmRows)), dim3(256), 0,
+                           stream, n, m, k, reinterpret_cast<const double*>(b), ldb, a, qk, qj,
+                           alpha, beta, C, (long long)ldc, 1LL);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((gemm_tsm_kernel<EB, EA>), dim3(gp_ceil_div(n, kTsmRows)), dim3(256), 0,
                        stream, n, m, k, b, ldb, a, qk, qj, alpha, beta, C, (long long)ldc, 1LL);
   }

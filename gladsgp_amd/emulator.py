@@ -137,7 +137,13 @@ class EmulatorData:
             mu = torch.as_tensor(_np(y_mean), dtype=F64, device=self.device).contiguous()
             sd = torch.as_tensor(_np(y_sd), dtype=F64, device=self.device).contiguous()
         sd_.y_mean, sd_.y_sd = mu, sd
-        sd_.y_std = blas.standardize(sd_.y_dev, mu, sd)
+        # rows padded to a multiple of 16 doubles (128 B): every row of the ensemble starts
+        # 16-B aligned, so the randomized SVD's ensemble-streaming products read it with 16-B
+        # loads (blas.hip tsk16 / tsm16); y_std is a (n x ny) view of the padded buffer
+        n, ny = sd_.y_dev.shape
+        ld = (ny + 15) // 16 * 16
+        out = torch.empty((n, ld), dtype=F64, device=sd_.y_dev.device)[:, :ny]
+        sd_.y_std = blas.standardize(sd_.y_dev, mu, sd, out=out)
 
     def create_K_basis(self, K):
         """Set the PCA basis K (P x ny) — SEPIA create_K_basis (model.py:102)."""

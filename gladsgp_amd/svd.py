@@ -183,7 +183,9 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
     # a float32 X stays float32 on the device: the GEMMs that stream it (gp_gemm_ex) widen it
     # exactly as they load it, so there is no fp64 copy of the ensemble (5.5 GB at the fit's
     # 512 x 1,347,945) and the products are bit-identical to those of an fp64 copy
-    Xt = _to_device(X, dev).contiguous()
+    Xt = _to_device(X, dev)
+    if not (Xt.dim() == 2 and Xt.stride(1) == 1 and Xt.stride(0) >= Xt.shape[1]):
+        Xt = Xt.contiguous()        # (a row-strided view -- the padded y_std -- is read in place)
     m_rows, n_cols = Xt.shape
     if k is None:
         k = p

@@ -46,7 +46,10 @@ def test_gemm(dev, ta, tb, m, n, k):
                                    # the tall-skinny kernels (blas.hip ts_kind): tsk (long K,
                                    # ta = 1), tsm (K <= 1024, the big side C's rows / C^T's)
                                    (512, 25, 70001), (700, 7, 65537), (20001, 25, 300),
-                                   (25, 20001, 300), (32, 9000, 512)])
+                                   (25, 20001, 300), (32, 9000, 512),
+                                   # even leading dimensions: the fp64 runs take the 16-B
+                                   # tsk16 / tsm16 forms, the float32 runs the 8-B ones
+                                   (512, 25, 70000), (20000, 25, 300)])
 def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
     """gp_gemm_ex with a float32 A and/or B (widened on load) equals gp_gemm_ex / gp_dgemm on
     fp64 copies of the same values bit for bit, split-K shapes included (512 x 25 x 40000 is
@@ -72,6 +75,42 @@ def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
     ref = 0.7 * ((A.T if ta else A).astype(np.float64) @ (B.T if tb else B)) - 1.3 * C0
     np.testing.assert_allclose(res[(0, 0)], ref, rtol=1e-12,
                                atol=1e-12 * np.sqrt(k) * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("kind", ["tsk", "tsm", "tsm_t"])
+@pytest.mark.parametrize("big", [70001, 20001])
+def test_tall_skinny_padded_ld_matches_unpadded(dev, kind, big):
+    """The ensemble's padded row stride (emulator.standardize_y) selects the 16-B tall-skinny
+    forms (blas.hip tsk16 / tsm16); they equal the 8-B forms on an unpadded copy bit for bit,
+    odd lengths (a 16-B pair straddling the end, zeroed) included, and numpy within 1e-12."""
+    from gladsgp_amd.blas import CM, gemm
+    if kind == "tsk" and big < 65536:
+        pytest.skip("tsk needs K >= 65536")
+    rng = np.random.default_rng(big + len(kind))
+    runs, r = 300 if kind != "tsk" else 512, 25
+    X = rng.standard_normal((runs, big))                 # C-order ensemble: runs x locations
+    ld = (big + 15) // 16 * 16
+    pad = torch.full((runs, ld), float("nan"), dtype=torch.float64, device=dev)
+    pad[:, :big] = _t(X, dev)
+    Xp = CM(pad, big, runs, ld)                          # (locations x runs), padded
+    Xu = CM(_t(X, dev), big, runs, big)
+    if kind == "tsk":                                    # (runs x r) = X W
+        W = rng.standard_normal((big, r))
+        Wc = CM(_t(W.T.copy(), dev), big, r, big)
+        outs = [gemm(True, False, M, Wc).logical().cpu().numpy() for M in (Xp, Xu)]
+        ref = X @ W
+    elif kind == "tsm":                                  # (locations x r) = X^T Y
+        Y = rng.standard_normal((runs, r))
+        Yc = CM(_t(Y.T.copy(), dev), runs, r, runs)
+        outs = [gemm(False, False, M, Yc).logical().cpu().numpy() for M in (Xp, Xu)]
+        ref = X.T @ Y
+    else:                                                # (r x locations) = Q^T X
+        Q = rng.standard_normal((runs, r))
+        Qc = CM(_t(Q.T.copy(), dev), runs, r, runs)
+        outs = [gemm(True, True, Qc, M).logical().cpu().numpy() for M in (Xp, Xu)]
+        ref = Q.T @ X
+    assert np.array_equal(outs[0], outs[1])
+    np.testing.assert_allclose(outs[0], ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
 
 
 def test_randomized_svd_float32_input_reads_no_fp64_copy(dev):
