@@ -478,8 +478,8 @@ __global__ __launch_bounds__(256, 3) void gemm_tsm_kernel(int M, int N, int K,
   }
 }
 
-// ---- 16-byte forms for fp64 operands whose rows / columns start 16-B aligned (the fit's
-// ensemble: y_std is allocated with a padded row stride, emulator.py standardize_y) ------------
+// ---- 16-byte form for fp64 ensembles whose rows start 16-B aligned (the fit's y_std is
+// allocated with a padded row stride, emulator.py standardize_y) -------------------------------
 // tsk16: as gemm_tsk_kernel, but 8 lanes read one row's 16 k as 16-B pairs (128 B per row, 8 rows
 // per load; 64 B with 8-B loads); X three groups ahead, W two (a 6-group unrolled ring).
 constexpr int kTsk16Pitch = 68;
@@ -569,90 +569,10 @@ __global__ __launch_bounds__(256, 2) void gemm_tsk16_kernel(int M, int N, int K,
       }
 }
 
-// tsm16: as gemm_tsm_kernel (128-row blocks, 32 rows per wave), but each lane reads rows
-// (2 li, 2 li + 1) of a column as one 16-B pair: MFMA tile e takes row 2 li + e (256 B per column
-// per load instead of 128).
-template <typename EQ>
-__global__ __launch_bounds__(256, 2) void gemm_tsm16_kernel(int M, int N, int K,
-                                                            const double* __restrict__ P, int ldp,
-                                                            const EQ* __restrict__ Q, long long qk,
-                                                            long long qj, double alpha,
-                                                            double beta, double* __restrict__ C,
-                                                            long long ci, long long cj) {
-  static_assert(kTsmRows == 128, "tsm16: 32 rows per wave");
-  __shared__ double cs[kTsmRows * 33];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int li = lane & 15, ks = lane >> 4;
-  const long long i0 = (long long)blockIdx.x * kTsmRows;
-  f64x4 acc[2][2];
-  acc[0][0] = acc[0][1] = acc[1][0] = acc[1][1] = zero4();
-  const long long r0 = i0 + w * 32 + 2 * li;             // rows r0, r0 + 1 (even: aligned pair)
-  const bool ok0 = r0 < M, ok1 = r0 + 1 < M;
-  const double* pcol = P + (ok0 ? r0 : 0);
-  const int jc0 = li, jc1 = 16 + li;
-  double2 a[kTsRing][4];
-  double bv[kTsRing][4][2];
-  auto load = [&](double2 (&ab)[4], double (&bb)[4][2], int k0) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k0 + 4 * u + ks;
-      const bool kok = k < K;
-      double2 v = make_double2(0.0, 0.0);
-      if (kok && ok0) v = *reinterpret_cast<const double2*>(pcol + (long long)k * ldp);
-      if (!ok1) v.y = 0.0;
-      ab[u] = v;
-      bb[u][0] = (kok && jc0 < N) ? static_cast<double>(Q[k * qk + jc0 * qj]) : 0.0;
-      bb[u][1] = (kok && jc1 < N) ? static_cast<double>(Q[k * qk + jc1 * qj]) : 0.0;
-    }
-  };
-#pragma unroll
-  for (int q = 0; q < kTsRing - 1; ++q) load(a[q], bv[q], 16 * q);
-  for (int k0 = 0; k0 < K; k0 += 16 * kTsRing) {
-    static_for<0, kTsRing, 1>([&](auto QQ) {
-      constexpr int q = decltype(QQ)::value;
-      const int kq = k0 + 16 * q;
-      if (kq >= K) return;
-      const int kn = kq + 16 * (kTsRing - 1);
-      if (kn < K) load(a[(q + kTsRing - 1) % kTsRing], bv[(q + kTsRing - 1) % kTsRing], kn);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc[0][0] = mfma16x16x4(a[q][u].x, bv[q][u][0], acc[0][0]);
-        acc[0][1] = mfma16x16x4(a[q][u].x, bv[q][u][1], acc[0][1]);
-        acc[1][0] = mfma16x16x4(a[q][u].y, bv[q][u][0], acc[1][0]);
-        acc[1][1] = mfma16x16x4(a[q][u].y, bv[q][u][1], acc[1][1]);
-      }
-    });
-  }
-  // tile e, MFMA row v = ks + 4q is block row w*32 + 2v + e
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        cs[(w * 32 + 2 * (ks + 4 * q) + e) * 33 + 16 * jt + li] = acc[e][jt][q];
-  __syncthreads();
-  const int rows = (int)min((long long)kTsmRows, M - i0);
-  if (cj == 1) {
-    for (int e = threadIdx.x; e < rows * N; e += 256) {
-      const int r = e / N, j = e - r * N;
-      double* cp = C + (i0 + r) * ci + j;
-      const double v = alpha * cs[r * 33 + j];
-      *cp = (beta == 0.0) ? v : fma(beta, *cp, v);
-    }
-  } else {
-    for (int e = threadIdx.x; e < rows * N; e += 256) {
-      const int j = e / rows, r = e - j * rows;
-      double* cp = C + (i0 + r) * ci + j * cj;
-      const double v = alpha * cs[r * 33 + j];
-      *cp = (beta == 0.0) ? v : fma(beta, *cp, v);
-    }
-  }
-}
-
-// 16-B forms apply to an fp64 big operand with 16-B aligned base and an even leading dimension
-// (and, for tsm16, padded columns: a pair never reads past the allocation -- an even ldp >= M
-// rounds M up inside it)
+// The 16-B form applies to an fp64 big operand with a 16-B aligned base and an even leading
+// dimension (a pair never reads past the row: an even ldp >= len rounds len up inside it).
+// (A 16-B tsm, each lane reading rows 2i, 2i + 1 of a column, ran 2.4 vs 1.6 ms on the fit's
+// products at its occupancy of 2 blocks per CU instead of 3: profiles/r05/r05j_prof_pca.log.)
 template <typename E>
 bool ts_vec_ok(const E* p, int ld, int len) {
   return sizeof(E) == 8 && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && (ld & 1) == 0 &&
@@ -726,27 +646,11 @@ hipError_t launch_ts(int kind, int transa, int transb, int m, int n, int k, doub
   if (kind == 2) {
     // C(i, j) = sum_k A[i + k*lda] opB(k, j), C[i + j*ldc]
     const long long qk = transb ? ldb : 1, qj = transb ? 1 : ldb;
-    if constexpr (sizeof(EA) == 8) {
-      if (ts_vec_ok(a, lda, m)) {
-        hipLaunchKernelGGL((gemm_tsm16_kernel<EB>), dim3(gp_ceil_div(m, kTsmRows)), dim3(256), 0,
-                           stream, m, n, k, reinterpret_cast<const double*>(a), lda, b, qk, qj,
-                           alpha, beta, C, 1LL, (long long)ldc);
-        return hipGetLastError();
-      }
-    }
     hipLaunchKernelGGL((gemm_tsm_kernel<EA, EB>), dim3(gp_ceil_div(m, kTsmRows)), dim3(256), 0,
                        stream, m, n, k, a, lda, b, qk, qj, alpha, beta, C, 1LL, (long long)ldc);
   } else {
     // C^T(j, i) = sum_k B[j + k*ldb] opA(i, k), C[i + j*ldc]: the big operand is B
     const long long qk = transa ? 1 : lda, qj = transa ? lda : 1;
-    if constexpr (sizeof(EB) == 8) {
-      if (ts_vec_ok(b, ldb, n)) {
-        hipLaunchKernelGGL((gemm_tsm16_kernel<EA>), dim3(gp_ceil_div(n, kTsmRows)), dim3(256), 0,
-                           stream, n, m, k, reinterpret_cast<const double*>(b), ldb, a, qk, qj,
-                           alpha, beta, C, (long long)ldc, 1LL);
-        return hipGetLastError();
-      }
-    }
     hipLaunchKernelGGL((gemm_tsm_kernel<EB, EA>), dim3(gp_ceil_div(n, kTsmRows)), dim3(256), 0,
                        stream, n, m, k, b, ldb, a, qk, qj, alpha, beta, C, (long long)ldc, 1LL);
   }

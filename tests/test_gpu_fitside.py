@@ -47,8 +47,8 @@ def test_gemm(dev, ta, tb, m, n, k):
                                    # ta = 1), tsm (K <= 1024, the big side C's rows / C^T's)
                                    (512, 25, 70001), (700, 7, 65537), (20001, 25, 300),
                                    (25, 20001, 300), (32, 9000, 512),
-                                   # even leading dimensions: the fp64 runs take the 16-B
-                                   # tsk16 / tsm16 forms, the float32 runs the 8-B ones
+                                   # even leading dimensions: the fp64 tsk runs take the
+                                   # 16-B tsk16 form, the float32 runs the 8-B one
                                    (512, 25, 70000), (20000, 25, 300)])
 def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
     """gp_gemm_ex with a float32 A and/or B (widened on load) equals gp_gemm_ex / gp_dgemm on
@@ -80,9 +80,10 @@ def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
 @pytest.mark.parametrize("kind", ["tsk", "tsm", "tsm_t"])
 @pytest.mark.parametrize("big", [70001, 20001])
 def test_tall_skinny_padded_ld_matches_unpadded(dev, kind, big):
-    """The ensemble's padded row stride (emulator.standardize_y) selects the 16-B tall-skinny
-    forms (blas.hip tsk16 / tsm16); they equal the 8-B forms on an unpadded copy bit for bit,
-    odd lengths (a 16-B pair straddling the end, zeroed) included, and numpy within 1e-12."""
+    """The ensemble's padded row stride (emulator.standardize_y) selects the 16-B tsk form
+    (blas.hip tsk16); every tall-skinny product on the padded ensemble equals the one on an
+    unpadded copy bit for bit, odd lengths (a 16-B pair straddling the row end, zeroed)
+    included, and numpy within 1e-12."""
     from gladsgp_amd.blas import CM, gemm
     if kind == "tsk" and big < 65536:
         pytest.skip("tsk needs K >= 65536")

@@ -1,7 +1,8 @@
 """Debug probe (not a test): what do the fit's ensemble-streaming products reach against plain
-streaming reads of the same 5.5 GB on this box?  X = (512 x 1,347,945) fp64 C-order, W =
-(1,347,945 x 25).  Times (median of 5, HIP events): torch X.sum() (a read of X), torch X @ W
-(hipBLAS dgemm), gp_gemm_ex's tsk (X W) and tsm (X^T Y, Y 512 x 25).
+streaming reads of the same 5.5 GB on this box?  X = (512 x 1,347,945) fp64 rows padded to 128 B
+(as emulator.standardize_y allocates y_std) and unpadded.  Times (median of 5, HIP events):
+X.sum() (a read of X), gp_gemm_ex's tsk (X W: W fp64 column-major = the fit's Z, and W float32
+row-major = the fit's Omega) and tsm (X^T Y, Q^T X).
 
     python tools/dbg/ts_probe.py
 """
@@ -16,10 +17,9 @@ from gladsgp_amd.blas import CM, gemm  # noqa: E402
 
 dev = torch.device("cuda:0")
 m, ny, r = 512, 1347945, 25
-X = torch.rand((m, ny), dtype=torch.float64, device=dev)
-W = torch.rand((ny, r), dtype=torch.float64, device=dev)
-Y = torch.rand((m, r), dtype=torch.float64, device=dev)
-GB = X.numel() * 8 / 1e9
+ld = (ny + 15) // 16 * 16
+Xpad = torch.rand((m, ld), dtype=torch.float64, device=dev)[:, :ny]
+GB = m * ny * 8 / 1e9
 
 
 def t(fn, reps=5):
@@ -36,15 +36,18 @@ def t(fn, reps=5):
     return float(np.median(ts))
 
 
-Xc = CM.of_rowmajor(X)                 # (ny x m), ld = ny
-Wt = W.t().contiguous()                # (25 x ny) C-order = column-major (ny x 25), ld = ny
-Wc = CM(Wt, ny, r, ny)
-Yt = Y.t().contiguous()
-Yc = CM(Yt, m, r, m)
-rows = []
-rows.append(("X.sum() (read X)", t(lambda: X.sum())))
-rows.append(("torch X @ W (hipBLAS)", t(lambda: X @ W)))
-rows.append(("gp tsk X W  (gemm(1,0))", t(lambda: gemm(True, False, Xc, Wc))))
-rows.append(("gp tsm X^T Y (gemm(0,0))", t(lambda: gemm(False, False, Xc, Yc))))
+Wz = CM.empty(ny, r, dev)                               # the fit's Z: fp64 (ny x r), ld = ny
+Wz.t.uniform_()
+Om = CM.of_rowmajor(torch.rand((ny, r), device=dev, dtype=torch.float32))   # (r x ny), ld = r
+Y = CM.empty(m, r, dev)
+Y.t.uniform_()
+rows = [("X.sum() (read X, padded)", t(lambda: Xpad.sum()))]
+for name, X in (("padded", Xpad), ("unpadded", Xpad.contiguous())):
+    Xc = CM.of_rowmajor(X)
+    rows.append((f"tsk X Z      [{name}]", t(lambda: gemm(True, False, Xc, Wz))))
+    rows.append((f"tsk X Omega  [{name}]", t(lambda: gemm(True, True, Xc, Om))))
+    rows.append((f"tsm X^T Y    [{name}]", t(lambda: gemm(False, False, Xc, Y))))
+    rows.append((f"tsm Q^T X^T  [{name}]", t(lambda: gemm(True, True, Y, Xc))))
+    del Xc
 for name, ms in rows:
     print(f"{name:28s} {ms:7.3f} ms  {GB / ms:6.2f} TB/s ({GB / ms / 8:.3f} of 8 TB/s)", flush=True)
