@@ -156,6 +156,11 @@ constexpr int kXcdPanels = TRMM_XCD_PANELS;
 #ifndef TRMM_PAIR_MIX
 #define TRMM_PAIR_MIX 0
 #endif
+// Diagonal-block steps (timing experiments only; 0 is the library): 1 = every MFMA of the step
+// (exact for the padded layout, whose upper triangle is zero), 2 = none (wrong results)
+#ifndef TRMM_DIAG_MODE
+#define TRMM_DIAG_MODE 0
+#endif
 
 // The tile-packed L^-1 (GPFIT_LINV_PACKED, the single-GP broadcast's payload): column k of the
 // padded npad x npad L^-1 from row 16 floor(k / 16) on, columns one after another, so every
@@ -326,7 +331,9 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
         else if (nst > BI / BK) issue(L, 0, smem + ((s + 1) & 1) * STAGE);
         else if (pass + 1 < npass)               // (a diagonal-only first tile) next tile's
           issue(Lb + Isecond * BI, first_step(Isecond), smem);   // first stage
-        if (s <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, s);
+        if (TRMM_DIAG_MODE == 1) trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
+        else if (TRMM_DIAG_MODE == 0 && s <= 7 - wr)
+          trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, s);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
@@ -354,7 +361,9 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
         else if (pass + 1 < npass)               // next tile's first stage
           issue(Lb + Isecond * BI, first_step(Isecond), smem);
         const int t = s - s_diag;               // the wave's last row tile is 7 - wr
-        if (t <= 7 - wr) trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, t);
+        if (TRMM_DIAG_MODE == 1) trmm_stage<false>(cur, cur + ASTAGE, acc, wr, wc, li, lk, 0);
+        else if (TRMM_DIAG_MODE == 0 && t <= 7 - wr)
+          trmm_stage<true>(cur, cur + ASTAGE, acc, wr, wc, li, lk, t);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
