@@ -161,6 +161,9 @@ constexpr int kXcdPanels = TRMM_XCD_PANELS;
 #ifndef TRMM_DIAG_MODE
 #define TRMM_DIAG_MODE 0
 #endif
+#ifndef TRMM_UNIT_MAP
+#define TRMM_UNIT_MAP 1
+#endif
 
 // The tile-packed L^-1 (GPFIT_LINV_PACKED, the single-GP broadcast's payload): column k of the
 // padded npad x npad L^-1 from row 16 floor(k / 16) on, columns one after another, so every
@@ -202,6 +205,7 @@ struct TrmmArgs {
   int Gp;                  // panels g < Gp: row-tile pair blocks (uniform 8 (NI + 1) K steps)
   int Gx;                  //   ... of which g < Gx (a multiple of 8 kXcdPanels) in the XCD order
   int Qc;                  // panels g >= Gp: one block per tile, longest tiles first
+  int umap;                // batched launches: XCD-local (problem, pair) units (trmm_sched)
 };
 
 // A tile's K order: the second tile of a row-tile pair (I < NI - 1 - I) runs its diagonal block
@@ -225,7 +229,16 @@ GP_DEV void trmm_block_tiles(int bid, const TrmmArgs& a, int& g, int& I0, int& I
   const int nA = a.Gp * NP;
   if (bid < nA) {
     int p;
-    if (bid < a.Gx * NP) {
+    if (a.umap) {
+      // unit u = (problem b, pair p) = u / NP, u % NP; XCD slot x takes units x, x + 8, ...,
+      // each over all NCt panels of the launch in turn (t = bid / 8): one XCD's resident blocks
+      // share one problem's pair p, i.e. two row tiles of L^-1 (<= 2 MB at n = 1024), where
+      // problem-major panels spread a whole 8 MB L^-1 over every XCD's 4 MB L2
+      const int x = bid & 7, t = bid >> 3, q = t / a.NCt;
+      const int u = x + 8 * q, C = t - q * a.NCt;
+      p = u % NP;
+      g = (u / NP) * a.NCt + C;
+    } else if (bid < a.Gx * NP) {
       const int x = bid & 7, t = bid >> 3, per = kXcdPanels * NP;
       const int grp = t / per, j = t - grp * per;
       p = j / kXcdPanels;
@@ -743,6 +756,9 @@ void trmm_sched(TrmmArgs& a, int batch, int slots) {
   a.Qc = (int)(G - Gp);
   const int grp = 8 * kXcdPanels;
   a.Gx = grp > 0 ? (a.Gp / grp) * grp : 0;
+  // XCD-local units for batches: every (problem, pair) unit spans whole launches' panels, and
+  // the units split evenly over the 8 XCD slots
+  a.umap = (TRMM_UNIT_MAP && batch > 1 && Gp == G && ((long long)batch * NP) % 8 == 0) ? 1 : 0;
 }
 
 // The last chunk's TRMM runs merged with the one before it when its blocks fill less than one
