@@ -161,8 +161,11 @@ constexpr int kXcdPanels = TRMM_XCD_PANELS;
 #ifndef TRMM_DIAG_MODE
 #define TRMM_DIAG_MODE 0
 #endif
+// XCD-local (problem, pair) units for batched launches (A/B build only): C4 TRMM 4.090 vs
+// 4.105-4.125 ms per launch, but 9.44 vs 5.47 GB of fabric traffic per launch (every K* panel
+// fetched by four XCDs; profiles/r05/r05m_umap.log, r05n_pmc_c4.log): not the default
 #ifndef TRMM_UNIT_MAP
-#define TRMM_UNIT_MAP 1
+#define TRMM_UNIT_MAP 0
 #endif
 
 // The tile-packed L^-1 (GPFIT_LINV_PACKED, the single-GP broadcast's payload): column k of the
