@@ -196,10 +196,13 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
         omega = legacy_normal_f32((n_cols, r))
     Om = _to_device(omega, dev).contiguous()      # float32 (as drawn) or float64
     Xc = CM.of_rowmajor(Xt)          # (n_cols x m_rows), ld = n_cols
-    # Omega column-major (n_cols x r, ld = n_cols): the tall-skinny X Omega then reads each of
-    # its r columns as a contiguous run; read row-major (transb) the same product ran 2.15 vs
-    # 1.47 ms at the fit's shape (profiles/r05/r05k_ts_probe.log).  Same values, same sums.
-    Oc = CM(Om.t().contiguous(), n_cols, r, max(n_cols, 1))
+    # Omega widened to fp64 (exactly) and column-major (n_cols x r, ld = n_cols) in one copy:
+    # the tall-skinny X Omega with a float32 W ran 2.15-2.51 ms against 1.31-1.47 with an fp64
+    # one at the fit's shape (profiles/r05/r05k_ts_probe.log, r05l_prof_pca.log).  The kernel
+    # widens a float32 operand exactly on load, so the sums are the same bits either way.
+    Ow = torch.empty((r, n_cols), dtype=torch.float64, device=Om.device)
+    Ow.copy_(Om.t())
+    Oc = CM(Ow, n_cols, r, max(n_cols, 1))
     Y = gemm(True, False, Xc, Oc)    # (m_rows x r) = X Omega
     for _ in range(q):
         Z = gemm(False, False, Xc, Y)    # (n_cols x r) = X^T Y
