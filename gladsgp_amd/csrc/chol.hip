@@ -2085,7 +2085,7 @@ static bool pp_eligible(int n, int batch, int resident) {
 // scratch (ldx = 64).
 static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx, long long sX,
                      int batch, int* info, double* logdet, bool inv, char* scr, int resident,
-                     hipStream_t stream) {
+                     hipStream_t stream, GpfitPre pre = GpfitPre()) {
   const int N = gp_ceil_div(n, NB);
   const PPScratch s = pp_scratch(n, batch, inv);
   const int grid = (int)(s.ntasks < resident ? s.ntasks : resident);
@@ -2099,6 +2099,10 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
                      inv ? 1 : 0, lead, kPPXDelay, head, (long long)(s.flag_bytes / sizeof(int)),
                      info, logdet, flags, s.fstride, budget < 0 ? 1 : 0);
   GP_CK(hipGetLastError());
+  if (pre.fn) {
+    const int prc = pre.fn(pre.arg);
+    if (prc) return prc;
+  }
   PPArgs P;
   P.A = A; P.sA = sA; P.lda = lda;
   P.X = X; P.sX = sX; P.ldx = ldx;
@@ -2182,10 +2186,10 @@ static int potrf_args(const double* A, int n, int lda, long long strideA, int ba
 int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
                           int ldinv, long long strideInv, int batch, int* info, double* logdet,
                           void* ws, long long ws_bytes, hipStream_t stream, int k_ev,
-                          hipEvent_t ev) {
+                          hipEvent_t ev, GpfitPre pre) {
   const int arc = potrf_inv_args(A, n, lda, strideA, Linv, ldinv, strideInv, batch);
   if (arc) return arc;
-  if (n == 0 || batch == 0) return 0;
+  if (n == 0 || batch == 0) return pre.fn ? pre.fn(pre.arg) : 0;
   const int npad = gp_padded_n(n);
   const int resident = pp_resident(stream);
   const bool pp = pp_eligible(n, batch, resident);
@@ -2193,6 +2197,10 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
     if (!ws || !ws_aligned(ws)) return -11;
     if (ws_bytes < gpfit_potrf_inv_ws_bytes(n, batch)) return -12;
   } else {   // (pp_factor's schedule kernel zeroes them)
+    if (pre.fn) {
+      const int prc = pre.fn(pre.arg);
+      if (prc) return prc;
+    }
     if (info) GP_CK(hipMemsetAsync(info, 0, sizeof(int) * batch, stream));
     if (logdet) GP_CK(hipMemsetAsync(logdet, 0, sizeof(double) * batch, stream));
   }
@@ -2207,7 +2215,7 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
     const int N = gp_ceil_div(n, NB);
     if (ev && k_ev >= 0 && k_ev < N) GP_CK(hipEventRecord(ev, stream));
     rc = pp_factor(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet, true,
-                   static_cast<char*>(ws), resident, stream);
+                   static_cast<char*>(ws), resident, stream, pre);
     if (rc == 0 && ev && !(k_ev >= 0 && k_ev < N)) GP_CK(hipEventRecord(ev, stream));
   } else {
     rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,

@@ -17,10 +17,18 @@ constexpr int GPFIT_POTRF_NB = 64;   // column block of gp_potrf_inv (chol.hip N
 // HBM-bound side work only when the factorisation turns latency-bound.  `ws` (256-B aligned)
 // holds gpfit_potrf_inv_ws_bytes(n, batch) bytes: the persistent factorisation's task list and
 // flags (nothing when n is beyond the persistent kernel's range).
+// `pre` (optional) is enqueued on `stream` ahead of the factorisation proper -- on the
+// persistent path after its schedule kernel (which reads nothing of A), so a caller can put the
+// Gram that produces A there and the schedule kernel's host-side setup no longer sits between
+// the Gram and the factorisation (gp_fit_predict).  A non-zero return aborts with that code.
+struct GpfitPre {
+  int (*fn)(void*) = nullptr;
+  void* arg = nullptr;
+};
 int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* Linv,
                           int ldinv, long long strideInv, int batch, int* info, double* logdet,
                           void* ws, long long ws_bytes, hipStream_t stream, int k_ev,
-                          hipEvent_t ev);
+                          hipEvent_t ev, GpfitPre pre = GpfitPre());
 long long gpfit_potrf_inv_ws_bytes(int n, int batch);
 
 // gp_gram_ardse writing only the lower triangle (j <= i); the upper triangle is left untouched.

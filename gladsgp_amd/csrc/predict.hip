@@ -1052,21 +1052,22 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
 
 // ------------------------------------------------------------------------------------------
 // gp_fit_predict: Gram -> Cholesky/L^-1 -> predict as one stream-ordered operation on `stream`.
-// With a context (gp_ctx_create) it forks over the context's two streams (equal priority):
-//   fact: Gram, the blocked factorisation (latency-bound, few CUs busy), then z = L^-1 w and
-//         per chunk, once that chunk's cross-covariance is done, the TRMM (all row tiles of the
-//         chunk, so its K* stays cached), and one mean / var pass over all m points (round 4
-//         ran this on a third stream; the event hop after the factorisation cost 16-20 us);
+// With a context (gp_ctx_create) the cross-covariance forks onto the context's stream:
+//   `stream`: the factorisation's schedule kernel, the Gram, the factorisation (latency-bound,
+//         few CUs busy), z = L^-1 w, and per chunk, once that chunk's cross-covariance is done,
+//         the TRMM (all row tiles of the chunk, so its K* stays cached), and one mean / var
+//         pass over all m points (round 4 forked the factorisation and the prediction onto
+//         streams of their own too; each event hop cost 16-27 us of the step);
 //   aux : the cross-covariance of every chunk (independent of the factorisation), CU-masked so
 //         that it leaves aux_free_cus CUs to the factorisation, from the factorisation's
 //         block step cross_start * n/64 on;
-// and joins back into `stream`.  Without a context every step runs in order on `stream`.
+// each TRMM waits for its chunk's event, which joins aux back.  Without a context every step
+// runs in order on `stream`.
 struct gp_ctx_s {
   int device = -1;
   double cross_start = 0.4;
   int aux_chunks = -1;           // cross-covariance chunks on aux (-1: all; gp_ctx_set_aux_chunks)
-  hipStream_t fact = nullptr, aux = nullptr;
-  hipEvent_t e_start = nullptr, e_done = nullptr;
+  hipStream_t aux = nullptr;
   hipEvent_t e_late = nullptr;   // the factorisation has turned latency-bound
   std::vector<hipEvent_t> e_chunk;  // after chunk ch's cross-covariance (grown on demand)
 };
@@ -1091,7 +1092,6 @@ hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
   if (e != hipSuccess) return e;
   c->cross_start = cross_start < 0 ? kCrossStart : cross_start;
   const int fr = aux_free_cus < 0 ? kAuxFreeCUs : aux_free_cus;
-  if ((e = hipStreamCreateWithFlags(&c->fact, hipStreamNonBlocking)) != hipSuccess) return e;
   // logical CU i sits on XCD i % 8 (measured with a CU-mask probe in round 1), so masking off
   // the low CUs reserves CUs evenly per XCD
   int ncu = 0;
@@ -1106,7 +1106,7 @@ hipError_t ctx_init(gp_ctx_s* c, double cross_start, int aux_free_cus) {
   } else if ((e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess) {
     return e;
   }
-  hipEvent_t* ev[3] = {&c->e_start, &c->e_done, &c->e_late};
+  hipEvent_t* ev[1] = {&c->e_late};
   for (hipEvent_t* p : ev)
     if ((e = hipEventCreateWithFlags(p, hipEventDisableTiming)) != hipSuccess) return e;
   return hipSuccess;
@@ -1118,13 +1118,13 @@ hipError_t ctx_fini(gp_ctx_s* c) {
   int dev0 = 0;
   keep(hipGetDevice(&dev0));
   if (c->device >= 0) keep(hipSetDevice(c->device));
-  hipStream_t st[2] = {c->fact, c->aux};
+  hipStream_t st[1] = {c->aux};
   for (hipStream_t x : st)
     if (x) {
       keep(hipStreamSynchronize(x));
       keep(hipStreamDestroy(x));
     }
-  hipEvent_t ev[3] = {c->e_start, c->e_done, c->e_late};
+  hipEvent_t ev[1] = {c->e_late};
   for (hipEvent_t x : ev)
     if (x) keep(hipEventDestroy(x));
   for (hipEvent_t x : c->e_chunk)
@@ -1199,23 +1199,44 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
       S->e_chunk.push_back(ev);
     }
   }
-  // the prediction runs on the factorisation's stream: z and the first TRMM follow the
-  // factorisation without a cross-stream hop (an event wait between pp_kernel and the trmv cost
-  // 16-20 us of every C3 step, profiles/r05/r05a_timeline.txt)
-  hipStream_t fact = S ? S->fact : stream, aux = S ? S->aux : stream, pred = fact;
-  if (S) {
-    GP_CK(hipEventRecord(S->e_start, stream));
-    GP_CK(hipStreamWaitEvent(fact, S->e_start, 0));
-  }
-  // fact: Gram -> Cholesky / L^-1, with e_late once the factorisation is latency-bound
-  rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, G, ldg, strideG, batch, fact);
-  if (rc) return rc;
+  // the factorisation and the prediction run on the caller's stream itself: z and the first
+  // TRMM follow the factorisation, and the next call's Gram the last TRMM, without a
+  // cross-stream hop (an event wait between pp_kernel and the trmv cost 16-20 us of every C3
+  // step, profiles/r05/r05a_timeline.txt; the fork / join through a context stream another
+  // ~27 us between steps, r05n_timeline.txt); only the cross-covariance forks onto aux
+  hipStream_t fact = stream, aux = S ? S->aux : stream, pred = fact;
+  // (the factorisation's schedule kernel,) Gram -> Cholesky / L^-1, with e_late once the
+  // factorisation is latency-bound.  The Gram is enqueued from inside the factorisation's
+  // setup, after its schedule kernel (GpfitPre): the schedule kernel's host-side preparation
+  // then overlaps the Gram instead of leaving the GPU idle between Gram and factorisation
+  // (16 us per C3 step, profiles/r05/r05n_timeline.txt)
   const int nblk = gp_ceil_div(n, GPFIT_POTRF_NB);
   const int k_late = S ? (int)(S->cross_start * nblk) : -1;
-  if (S && k_late <= 0) GP_CK(hipEventRecord(S->e_late, fact));
+  struct GramPre {
+    const double *X, *beta, *s, *delta;
+    double* G;
+    int ldx, ldbeta, n, d, ldg, batch;
+    long long strideG;
+    hipStream_t st;
+    hipEvent_t late;
+  } gp{X, beta, s, delta, G, ldx, ldbeta, n, d, ldg, batch, strideG, fact,
+       (S && k_late <= 0) ? S->e_late : nullptr};
+  GpfitPre pre;
+  pre.arg = &gp;
+  pre.fn = [](void* a) -> int {
+    const GramPre& g = *static_cast<const GramPre*>(a);
+    const int grc = gpfit_gram_lower(g.X, g.n, g.d, g.ldx, g.beta, g.ldbeta, g.s, g.delta, g.G,
+                                     g.ldg, g.strideG, g.batch, g.st);
+    if (grc) return grc;
+    if (g.late) {
+      const hipError_t er = hipEventRecord(g.late, g.st);
+      if (er != hipSuccess) return GPFIT_ERR_HIP - (int)er;
+    }
+    return 0;
+  };
   rc = gpfit_potrf_inv_event(G, n, ldg, strideG, Linv, ldinv, strideInv, batch, info, logdet,
                              w.pot, p.bytes - p.off_pot, fact, k_late > 0 ? k_late : -1,
-                             (S && k_late > 0) ? S->e_late : nullptr);
+                             (S && k_late > 0) ? S->e_late : nullptr, pre);
   if (rc) return rc;
   if (S) GP_CK(hipStreamWaitEvent(aux, S->e_late, 0));
   // chunks whose cross-covariance runs on aux, beside the factorisation and the earlier TRMMs
@@ -1243,10 +1264,7 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
                     return cross_chunk(p, ch, w.kt + (long long)ch * p.slab_elems, X, ldx, Xs,
                                        ldxs, n, m, d, beta, ldbeta, s, batch, pred);
                   }));
-  if (S) {
-    GP_CK(hipEventRecord(S->e_done, pred));
-    GP_CK(hipStreamWaitEvent(stream, S->e_done, 0));
-  }
+  // (every chunk's cross-covariance on aux is joined by the TRMM that waits for its event)
 #undef GP_CK
   return 0;
 }

@@ -237,8 +237,9 @@ int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
 
 /*
  * Execution context of gp_fit_predict, created and destroyed by the caller on the current
- * device: two streams (factorisation then prediction | cross-covariance) and their events (one
- * per test-point chunk after its cross-covariance, created on the first call that needs them).
+ * device: one stream for the cross-covariance (the factorisation and the prediction run on the
+ * caller's stream) and its events (one per test-point chunk after its cross-covariance,
+ * created on the first call that needs them).
  *   cross_start  : fraction of the factorisation's n/64 block steps after which the
  *                  cross-covariance starts (< 0: default 0.4; 0 = at once);
  *   aux_free_cus : CUs the cross-covariance stream leaves to the factorisation (CU mask;
@@ -262,11 +263,11 @@ int gp_ctx_set_aux_chunks(void* ctx, int nchunks);
  * Fit + predict in one call:
  *   G = gram(X) (caller buffer, L on return) -> L, L^-1, info, logdet (as gp_potrf_inv) ->
  *   mean / var at the m test points (as gp_predict).
- * With ctx == NULL every step runs in order on `stream`.  With a context it forks from
- * `stream` into the context's streams (Gram + factorisation, then z = L^-1 w and per chunk,
- * once that chunk's cross-covariance is done, its TRMM, and one mean/var pass | the
- * cross-covariance of every chunk, beside the factorisation (CU-masked if asked)) and joins
- * back: the caller sees one stream-ordered operation.  `ws` holds
+ * With ctx == NULL every step runs in order on `stream`.  With a context the cross-covariance
+ * of every chunk forks onto the context's stream, beside the factorisation (CU-masked if
+ * asked), while `stream` runs the Gram + factorisation, z = L^-1 w and per chunk, once that
+ * chunk's cross-covariance is done, its TRMM, then one mean/var pass: the caller sees one
+ * stream-ordered operation.  `ws` holds
  * gp_fit_predict_ws_bytes(n, m, batch, m_chunk) bytes (the factorisation's scratch included).
  * The prediction runs whatever info says: mean / var of a problem with info[b] != 0 are
  * unspecified (check info; -1 is an internal error, see the conventions).

@@ -5,4 +5,3 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_fitside.py tests/test_gpu_e
 rc=$?; tail -3 gpurun_out/r05l_pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python tools/prof_pca.py > gpurun_out/r05l_prof_pca.log 2>&1 || exit 1
 grep -E "gemm\(|init_model|randomized" gpurun_out/r05l_prof_pca.log | head -14
-AB_WORKLOADS="c4 c3" timeout -k 10 600 bash tools/ab_bench_libs.sh r05l_diag _ab/libgpfit_cur.so _ab/libgpfit_dm1.so _ab/libgpfit_dm2.so || exit 1
