@@ -2085,7 +2085,8 @@ static bool pp_eligible(int n, int batch, int resident) {
 // scratch (ldx = 64).
 static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx, long long sX,
                      int batch, int* info, double* logdet, bool inv, char* scr, int resident,
-                     hipStream_t stream, GpfitPre pre = GpfitPre()) {
+                     hipStream_t stream, GpfitPre pre = GpfitPre(),
+                     hipEvent_t ev_launch = nullptr) {
   const int N = gp_ceil_div(n, NB);
   const PPScratch s = pp_scratch(n, batch, inv);
   const int grid = (int)(s.ntasks < resident ? s.ntasks : resident);
@@ -2103,6 +2104,7 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
     const int prc = pre.fn(pre.arg);
     if (prc) return prc;
   }
+  if (ev_launch) GP_CK(hipEventRecord(ev_launch, stream));   // after the Gram, before pp_kernel
   PPArgs P;
   P.A = A; P.sA = sA; P.lda = lda;
   P.X = X; P.sX = sX; P.ldx = ldx;
@@ -2210,12 +2212,13 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
   int rc;
   if (pp) {
     // one launch, no block steps: an event asked for at a step inside the factorisation is
-    // recorded before the launch (whatever waits on it runs beside the whole factorisation),
+    // recorded just before the persistent launch, after the schedule kernel and `pre` (whatever
+    // waits on it runs beside the whole factorisation, not beside the Gram),
     // one asked for at k_ev >= N after it
     const int N = gp_ceil_div(n, NB);
-    if (ev && k_ev >= 0 && k_ev < N) GP_CK(hipEventRecord(ev, stream));
     rc = pp_factor(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet, true,
-                   static_cast<char*>(ws), resident, stream, pre);
+                   static_cast<char*>(ws), resident, stream, pre,
+                   (ev && k_ev >= 0 && k_ev < N) ? ev : nullptr);
     if (rc == 0 && ev && !(k_ev >= 0 && k_ev < N)) GP_CK(hipEventRecord(ev, stream));
   } else {
     rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,

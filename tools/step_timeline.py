@@ -6,7 +6,11 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "ardse_kernel" in r["Kernel_Name"]]
+# a step starts with the factorisation's schedule kernel (enqueued ahead of the Gram since
+# round 5), or with the Gram in older traces
+mark = "pp_schedule_kernel" if any("pp_schedule_kernel" in r["Kernel_Name"] for r in rows) \
+    else "ardse_kernel"
+starts = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
 seq = rows[starts[-2]:starts[-1]] if len(starts) > 1 else rows[starts[-1]:]
 
 
@@ -42,11 +46,11 @@ print(f"  prediction phase: {len(tr)} kernels, idle between them {gap / 1e3:.1f}
 if len(starts) > 2:
     per = [(int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
            for a, b in zip(starts, starts[1:])]
-    print(f"  step period (Gram to Gram) us: min {min(per):.1f} median "
+    print(f"  step period (step start to step start) us: min {min(per):.1f} median "
           f"{sorted(per)[len(per) // 2]:.1f} max {max(per):.1f} over {len(per)}")
     last_pred = max(int(r["End_Timestamp"]) for r in tr)
     nxt = rows[starts[-1]]
-    print(f"  last prediction kernel end -> next Gram start: "
+    print(f"  last prediction kernel end -> next step start: "
           f"{(int(nxt['Start_Timestamp']) - last_pred) / 1e3:.1f} us; between them:")
     for r in rows:
         s0 = int(r["Start_Timestamp"])
