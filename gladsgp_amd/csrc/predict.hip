@@ -831,7 +831,12 @@ hipError_t solve_all(const Plan& p, const WS& w, const LinvRef& L, const double*
         gpfit_prof_begin(GP_PROF_CROSS, stream);
         if ((e = cross(c)) != hipSuccess) return e;
         gpfit_prof_end(GP_PROF_CROSS, stream);
-      } else if (ready && c > 0 && (e = hipStreamWaitEvent(stream, ready[c], 0)) != hipSuccess) {
+      } else if (ready && c == 1 &&
+                 (e = hipStreamWaitEvent(stream, ready[late - 1], 0)) != hipSuccess) {
+        // chunk 1 waits for the last aux chunk, which (aux is in order) covers every later
+        // one: one queue barrier instead of one per launch (~4 us each beside the 1.7-1.9 us
+        // kernel boundary, profiles/r05/r05p_timeline.txt); those chunks are long done when
+        // the second TRMM is reached
         return e;
       }
     }

@@ -2,7 +2,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 R0=$(pwd)
-timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 250 --timeout-method thread > gpurun_out/r05p_pytest.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_gpu_sched.py tests/test_gpu_c3.py tests/test_gpu_c4.py tests/test_gpu_rccl.py -x -q --timeout 250 --timeout-method thread > gpurun_out/r05p_pytest.log 2>&1
 rc=$?; tail -2 gpurun_out/r05p_pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 bash tools/ab_bench_libs.sh r05p_ab _ab/libgpfit_cur.so _ab/libgpfit_hop.so || exit 1
 cd /tmp && export TMPDIR=/tmp
