@@ -37,7 +37,7 @@ for path in sys.argv[1:]:
     libs.append((os.path.basename(path), h))
 dev = torch.device("cuda:0")
 st = torch.cuda.current_stream(dev).cuda_stream
-for n, B in ((4096, 1), (1024, 32), (2048, 4)):
+for n, B in ((4096, 1), (1024, 32), (2048, 4), (512, 24)):
     X = torch.as_tensor(np.random.default_rng(0).random((n, 8)), device=dev)
     betas = torch.as_tensor(np.stack([np.random.default_rng(10 + b).uniform(0.5, 5, 8)
                                       for b in range(B)]), device=dev)
