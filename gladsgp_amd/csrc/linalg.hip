@@ -77,62 +77,6 @@ __global__ __launch_bounds__(256) void nll_reduce_kernel(const double* __restric
   }
 }
 
-// gp_loglik's tail in one launch, one workgroup per problem: z = L^-1 w in 64-row passes (the
-// trmv_kernel's row / k-slice arithmetic), each pass's z_r^2 added to thread r % 64's running
-// sum, then the 64 sums in a fixed tree and nll_reduce_kernel's epilogue.  Replaces trmv_kernel
-// + nll_reduce_kernel (8.8 + 4.6 us per Metropolis group at 24 x n = 512 plus a kernel
-// boundary, profiles/r05/r05t_prof_fit.txt); deterministic.
-__global__ __launch_bounds__(1024) void loglik_tail_kernel(const double* __restrict__ Linv,
-                                                           int ld, long long sL,
-                                                           const double* __restrict__ w,
-                                                           int ldw, int n,
-                                                           const double* __restrict__ logdet,
-                                                           const int* __restrict__ info,
-                                                           double sign, double* __restrict__ nll,
-                                                           int* __restrict__ status,
-                                                           int* __restrict__ info_out) {
-  const int b = blockIdx.x;
-  const int rl = threadIdx.x & 63, ks = threadIdx.x >> 6;
-  const double* L = Linv + b * sL;
-  const double* wb = w + (long long)b * ldw;
-  __shared__ double red[kTrmvSlices][64];
-  double sq = 0.0;                                   // thread rl (ks == 0): sum of its z_r^2
-  for (int rb = 0; rb < n; rb += 64) {
-    const int r = rb + rl;
-    double acc0 = 0.0, acc1 = 0.0;
-    const int kend = min(rb + 64, n);
-    if (r < n) {
-      int k = ks;
-      for (; k + kTrmvSlices < kend; k += 2 * kTrmvSlices) {
-        acc0 = fma(L[r + (long long)k * ld], wb[k], acc0);
-        acc1 = fma(L[r + (long long)(k + kTrmvSlices) * ld], wb[k + kTrmvSlices], acc1);
-      }
-      if (k < kend) acc0 = fma(L[r + (long long)k * ld], wb[k], acc0);
-    }
-    red[ks][rl] = acc0 + acc1;
-    __syncthreads();
-    if (ks == 0 && r < n) {
-      double z = 0.0;
-#pragma unroll
-      for (int q = 0; q < kTrmvSlices; ++q) z += red[q][rl];
-      sq = fma(z, z, sq);
-    }
-    __syncthreads();
-  }
-  if (ks == 0) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off, 64);
-    if (rl == 0) {
-      const double v = 0.5 * sq + 0.5 * logdet[b];
-      const int f = info ? info[b] : 0;
-      nll[b] = f < 0 ? __builtin_nan("") : sign * (f > 0 ? __builtin_huge_val() : v);
-      if (info_out) info_out[b] = f;
-      if (f < 0 && status)
-        __hip_atomic_fetch_or(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 }  // namespace
 
 hipError_t gpfit_trmv_rows_launch(const double* Linv, int ld, long long sL, const double* w,
@@ -260,10 +204,12 @@ extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* b
   rc = gpfit_potrf_inv_event(c.G, n, n, (long long)n * n, c.Linv, npad, (long long)npad * npad,
                              batch, c.info, c.logdet, c.pot, c.pot_bytes, stream, -1, nullptr);
   if (rc) return rc;
-  hipLaunchKernelGGL(loglik_tail_kernel, dim3(batch), dim3(1024), 0, stream, c.Linv, npad,
-                     (long long)npad * npad, w, ldw, n, c.logdet, (const int*)c.info, -1.0, ll,
-                     c.status, info);
-  hipError_t e = hipGetLastError();
+  hipError_t e = gpfit_trmv_launch(c.Linv, npad, (long long)npad * npad, w, ldw, c.z, n, n, n,
+                                   batch, stream);
+  if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
+  hipLaunchKernelGGL(nll_reduce_kernel, dim3(batch), dim3(256), 0, stream, c.z, n, n, c.logdet,
+                     (const int*)c.info, -1.0, ll, c.status, info);
+  e = hipGetLastError();
   if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e;
   return 0;
 }
