@@ -442,6 +442,9 @@ GP_DEV void leaf16(lds_double* T, lds_double* U, int o, lds_double* piv) {
   if (lane < 16) piv[o + c] = colpiv;
 }
 
+#ifndef LEAF_MASKED
+#define LEAF_MASKED 0
+#endif
 #ifndef PP_LEAF_BLOCKED
 #define PP_LEAF_BLOCKED 1   // 0: leaf16 (one MFMA per column), 1: leaf16_blocked
 #endif
@@ -487,6 +490,12 @@ GP_DEV void leaf16_blocked(lds_double* T, lds_double* U, int o, lds_double* piv)
       const double p = readlane_f64(t[jj], j);
       colpiv = (c == j) ? p : colpiv;
       rowpiv[q] = (r0 == jj) ? p : rowpiv[q];
+#if LEAF_MASKED
+      // row j masked to the columns it still updates (c > j) while the pivot's reciprocal is
+      // formed: the update below then needs no select on its dependency chain (columns c <= j
+      // get fma(-m, 0, t) = t)
+      const double tjm = (c > j) ? t[jj] : 0.0;
+#endif
       if constexpr (j < 15) {
         // 1 / p_j: v_rcp_f64's estimate (~2^-26: 1e-8 residuals alone) + one Newton step, as
         // accurate as two here (|LL^T - G| and |L^-1 L - I| unchanged on the micro-benchmark's
@@ -502,7 +511,11 @@ GP_DEV void leaf16_blocked(lds_double* T, lds_double* U, int o, lds_double* piv)
         static_for<jj + 1, 4, 1>([&](auto K) {
           constexpr int k = decltype(K)::value;
           const double m = readlane_f64(t[jj], 4 * q + k) * rp;     // A[j][4q+k] / p_j
+#if LEAF_MASKED
+          t[k] = fma(-m, tjm, t[k]);
+#else
           t[k] = (c > j) ? fma(-m, t[jj], t[k]) : t[k];
+#endif
           tw[k] = fma(-m, tw[jj], tw[k]);
         });
       }
