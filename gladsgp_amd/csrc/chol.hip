@@ -443,7 +443,7 @@ GP_DEV void leaf16(lds_double* T, lds_double* U, int o, lds_double* piv) {
 }
 
 #ifndef LEAF_MASKED
-#define LEAF_MASKED 0
+#define LEAF_MASKED 1
 #endif
 #ifndef PP_LEAF_BLOCKED
 #define PP_LEAF_BLOCKED 1   // 0: leaf16 (one MFMA per column), 1: leaf16_blocked
