@@ -304,7 +304,13 @@ namespace {
 // exactly, as the general kernel does), so float32 and fp64 operands give the same bits.
 constexpr int kTskRows = 256;        // rows of C per tsk block (4 waves x 64)
 constexpr int kTskMinK = 1 << 16;
-constexpr int kTsmRows = 128;        // rows of the big dimension per tsm block (4 waves x 32)
+#ifndef TSM_ROWS
+#define TSM_ROWS 128
+#endif
+#ifndef TSM_OCC
+#define TSM_OCC 3
+#endif
+constexpr int kTsmRows = TSM_ROWS;   // rows of the big dimension per tsm block (4 waves x 32)
 constexpr int kTsmMaxK = 1024;   // K of a tsm product (the number of runs)
 constexpr int kTsMaxN = 32;          // narrow side (two 16-wide MFMA column tiles)
 
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tsk_kernel(int M, int N, int K, i
 // L2: 100 KB at the fit's 512 x 25), C(i, j) = C[i*ci + j*cj].  The block's rows are written
 // through LDS as runs along whichever of i / j is contiguous in C.
 template <typename EP, typename EQ>
-__global__ __launch_bounds__(256, 3) void gemm_tsm_kernel(int M, int N, int K,
+__global__ __launch_bounds__(256, TSM_OCC) void gemm_tsm_kernel(int M, int N, int K,
                                                           const EP* __restrict__ P, int ldp,
                                                           const EQ* __restrict__ Q, long long qk,
                                                           long long qj, double alpha,
