@@ -298,19 +298,25 @@ namespace {
 //       32 B per load -- and reached 0.19-0.25 of HBM: profiles/r05/r05g_prof_pca.log.)
 //   tsm (C = X^T Y or Q^T X, the big side is the output): every block owns kTsmRows rows of the
 //       big dimension and the whole K <= kTsmMaxK (the narrow operand read through L1 / L2),
-//       three blocks per CU; the accumulators go through LDS so the output is written as
-//       contiguous runs.  (256-row blocks at one per CU reached 0.45 of HBM, r05g_prof_pca.log.)
+//       two blocks per CU; the accumulators go through LDS so the output is written as
+//       contiguous runs.
 // The operands' element types are template parameters (float32 X read as stored and widened
 // exactly, as the general kernel does), so float32 and fp64 operands give the same bits.
-constexpr int kTskRows = 256;        // rows of C per tsk block (4 waves x 64)
+#ifndef TSK_WAVES
+#define TSK_WAVES 4
+#endif
+constexpr int kTskWaves = TSK_WAVES;           // waves per tsk block, 64 rows each
+constexpr int kTskRows = 64 * kTskWaves;       // rows of C per tsk block
 constexpr int kTskMinK = 1 << 16;
+// 256 rows (4 waves x 64) at two blocks per CU: 0.53-0.56 of HBM on the fit's products, against
+// 0.42-0.47 at 128 x 3, 0.29-0.31 at 64 x 4, 0.48-0.49 at 512 x 1 (profiles/r05/r05w_tsm*.log)
 #ifndef TSM_ROWS
-#define TSM_ROWS 128
+#define TSM_ROWS 256
 #endif
 #ifndef TSM_OCC
-#define TSM_OCC 3
+#define TSM_OCC 2
 #endif
-constexpr int kTsmRows = TSM_ROWS;   // rows of the big dimension per tsm block (4 waves x 32)
+constexpr int kTsmRows = TSM_ROWS;   // rows of the big dimension per tsm block
 constexpr int kTsmMaxK = 1024;   // K of a tsm product (the number of runs)
 constexpr int kTsMaxN = 32;          // narrow side (two 16-wide MFMA column tiles)
 
@@ -324,12 +330,12 @@ constexpr int kTskPitch = 72; // tsk LDS transpose: doubles per k row of a wave'
 // C(i, j) = sum_k P(i, k) W(k, j) for i < M (P(i,k) = P[k + i*ldp], contiguous in k), j < N <= 32,
 // W(k, j) = W[k*wk + j*wj], k in this block's slice; partial C to part[slice][j*M + i].
 template <typename EP, typename EW>
-__global__ __launch_bounds__(256, 2) void gemm_tsk_kernel(int M, int N, int K, int kslice,
+__global__ __launch_bounds__(64 * kTskWaves, 8 / kTskWaves) void gemm_tsk_kernel(int M, int N, int K, int kslice,
                                                           const EP* __restrict__ P, int ldp,
                                                           const EW* __restrict__ W, long long wk,
                                                           long long wj, double* __restrict__ part) {
   constexpr int G = kTskKG, R = kTskRing, NQ = 64 * G / 64;   // NQ loads of one group per lane
-  __shared__ double xs[4 * G * kTskPitch];
+  __shared__ double xs[kTskWaves * G * kTskPitch];
   const int slice = blockIdx.x, rg = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 15, ks = lane >> 4;
@@ -491,13 +497,13 @@ __global__ __launch_bounds__(256, TSM_OCC) void gemm_tsm_kernel(int M, int N, in
 constexpr int kTsk16Pitch = 68;
 
 template <typename EW>
-__global__ __launch_bounds__(256, 2) void gemm_tsk16_kernel(int M, int N, int K, int kslice,
+__global__ __launch_bounds__(64 * kTskWaves, 8 / kTskWaves) void gemm_tsk16_kernel(int M, int N, int K, int kslice,
                                                             const double* __restrict__ P, int ldp,
                                                             const EW* __restrict__ W, long long wk,
                                                             long long wj,
                                                             double* __restrict__ part) {
   constexpr int G = 16, RX = 3, RW = 2;
-  __shared__ double xs[4 * G * kTsk16Pitch];
+  __shared__ double xs[kTskWaves * G * kTsk16Pitch];
   const int slice = blockIdx.x, rg = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 15, ks = lane >> 4;
@@ -596,10 +602,10 @@ int ts_kind(int transa, int transb, int m, int n, int k) {
   return 0;
 }
 
-// tsk's K slices: about two blocks per CU over all row groups, each slice a multiple of 16.
+// tsk's K slices: eight waves per CU over all row groups, each slice a multiple of 16.
 void tsk_shape(int m, int k, int& groups, int& slices, int& kslice) {
   groups = gp_ceil_div(m, kTskRows);
-  slices = max(1, 512 / groups);
+  slices = max(1, (2048 / kTskWaves) / groups);
   kslice = gp_ceil_div(gp_ceil_div(k, slices), 16) * 16;
   slices = gp_ceil_div(k, kslice);
 }
@@ -632,14 +638,14 @@ hipError_t launch_ts(int kind, int transa, int transb, int m, int n, int k, doub
     const long long wk = transb ? ldb : 1, wj = transb ? 1 : ldb;
     if constexpr (sizeof(EA) == 8) {
       if (ts_vec_ok(a, lda, k))
-        hipLaunchKernelGGL((gemm_tsk16_kernel<EB>), dim3(slices, groups), dim3(256), 0, stream,
+        hipLaunchKernelGGL((gemm_tsk16_kernel<EB>), dim3(slices, groups), dim3(64 * kTskWaves), 0, stream,
                            m, n, k, kslice, reinterpret_cast<const double*>(a), lda, b, wk, wj,
                            part);
       else
-        hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(256), 0, stream,
+        hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(64 * kTskWaves), 0, stream,
                            m, n, k, kslice, a, lda, b, wk, wj, part);
     } else {
-      hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(256), 0, stream, m,
+      hipLaunchKernelGGL((gemm_tsk_kernel<EA, EB>), dim3(slices, groups), dim3(64 * kTskWaves), 0, stream, m,
                          n, k, kslice, a, lda, b, wk, wj, part);
     }
     hipError_t e = hipGetLastError();
