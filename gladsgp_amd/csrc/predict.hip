@@ -153,9 +153,6 @@ GP_DEV void trmm_stage(const double* __restrict__ As, const double* __restrict__
 #define TRMM_XCD_PANELS 8
 #endif
 constexpr int kXcdPanels = TRMM_XCD_PANELS;
-#ifndef TRMM_PAIR_MIX
-#define TRMM_PAIR_MIX 0
-#endif
 // Diagonal-block steps (timing experiments only; 0 is the library): 1 = every MFMA of the step
 // (exact for the padded layout, whose upper triangle is zero), 2 = none (wrong results)
 #ifndef TRMM_DIAG_MODE
@@ -245,9 +242,6 @@ GP_DEV void trmm_block_tiles(int bid, const TrmmArgs& a, int& g, int& I0, int& I
       const int x = bid & 7, t = bid >> 3, per = kXcdPanels * NP;
       const int grp = t / per, j = t - grp * per;
       p = j / kXcdPanels;
-      // pair-order mixes (A/B builds only; every map is a bijection on (p, panel))
-      if (TRMM_PAIR_MIX == 1 && (grp & 1)) p = NP - 1 - p;
-      if (TRMM_PAIR_MIX == 2 && (j & 1)) p = NP - 1 - p;
       g = x + 8 * (grp * kXcdPanels + j % kXcdPanels);
     } else {
       const int r = bid - a.Gx * NP, Gr = a.Gp - a.Gx;
@@ -256,8 +250,8 @@ GP_DEV void trmm_block_tiles(int bid, const TrmmArgs& a, int& g, int& I0, int& I
     }
     I0 = a.NI - 1 - p;
     I1 = (I0 == p) ? -1 : p;
-    // (A/B build) the pair's diagonal-first tile first in every other block
-    if (TRMM_PAIR_MIX == 3 && I1 >= 0 && (bid & 8)) { I1 = I0; I0 = p; }
+    // (pair-order mixes -- reversed pairs in every other XCD group or block, or the pair's
+    // diagonal-first tile first -- measured no different, profiles/r05/r05f_ab.log)
   } else {
     const int t = bid - nA;
     const int q = t / a.Qc;
