@@ -133,6 +133,39 @@ __global__ void splitk_reduce_kernel(const double* __restrict__ part, int splits
   *c = (beta == 0.0) ? alpha * s : fma(alpha, s, beta * *c);
 }
 
+// The tsk products' reduction (hundreds of slices over a small C: 256 x 512 x 25 at the fit):
+// 32 outputs x 8 slice groups per block, group h summing its contiguous run of slices in order
+// with eight loads in flight, then the eight group sums added in group order (a fixed order:
+// deterministic).  splitk_reduce_kernel's thread per output summed 256 slices one load at a
+// time on 50 CUs: 74 us per product (profiles/r05/r05_pmc_ts.txt).
+constexpr int kRedGroups = 8;
+__global__ __launch_bounds__(256) void splitk_reduce_wide_kernel(
+    const double* __restrict__ part, int splits, int M, int N, double alpha, double beta,
+    double* __restrict__ C, int ldc) {
+  __shared__ double red[kRedGroups][33];
+  const int o = threadIdx.x & 31, h = threadIdx.x >> 5;
+  const long long MN = (long long)M * N;
+  const long long idx = (long long)blockIdx.x * 32 + o;
+  const int per = (splits + kRedGroups - 1) / kRedGroups;
+  const int p0 = min(splits, h * per), p1 = min(splits, p0 + per);
+  double s = 0.0;
+  if (idx < MN) {
+    const double* q = part + idx;
+#pragma unroll 8
+    for (int p = p0; p < p1; ++p) s += q[(long long)p * MN];
+  }
+  red[h][o] = s;
+  __syncthreads();
+  if (h == 0 && idx < MN) {
+    double t = red[0][o];
+#pragma unroll
+    for (int g = 1; g < kRedGroups; ++g) t += red[g][o];
+    const int gi = (int)(idx % M), gj = (int)(idx / M);
+    double* c = C + gi + (long long)gj * ldc;
+    *c = (beta == 0.0) ? alpha * t : fma(alpha, t, beta * *c);
+  }
+}
+
 int choose_splits(int M, int N, int K) {
   const int tiles = gp_ceil_div(M, TB) * gp_ceil_div(N, TB);
   int s = 1;
@@ -293,7 +326,7 @@ namespace {
 //       wave 64 rows (4 row tiles x 2 column tiles of 16 in MFMA accumulators).  X is loaded
 //       row-contiguous (8 lanes read 8 consecutive k of one row: 64 B per row, 8 rows per
 //       load), three K-groups ahead in registers, and transposed into the MFMA A layout through
-//       a wave-private LDS tile; partial C per slice, then splitk_reduce_kernel (fixed order:
+//       a wave-private LDS tile; partial C per slice, then splitk_reduce_wide_kernel (fixed order:
 //       deterministic).  (Round 5's first tsk loaded X straight into the A layout -- 16 rows x
 //       32 B per load -- and reached 0.19-0.25 of HBM: profiles/r05/r05g_prof_pca.log.)
 //   tsm (C = X^T Y or Q^T X, the big side is the output): every block owns kTsmRows rows of the
@@ -651,7 +684,7 @@ hipError_t launch_ts(int kind, int transa, int transb, int m, int n, int k, doub
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const long long tot = (long long)m * n;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(splitk_reduce_wide_kernel, dim3((unsigned)((tot + 31) / 32)), dim3(256), 0,
                        stream, part, slices, m, n, alpha, beta, C, ldc);
     return hipGetLastError();
   }
