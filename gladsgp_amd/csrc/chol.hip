@@ -1904,18 +1904,27 @@ GP_HD inline int pp_nkeys(int N, int lead, int xd) { return 4 * N - 1 + 4 * (lea
 // Also zeroes the launch's flag words (dequeue head + per-tile flags) and info / logdet (in
 // place of three memset launches ahead of it: ~30 us of a C3 step); `preset_abort` (the
 // gp_set_poll_budget test hook) then marks every problem as having spent its poll budget.
+// Block b of the grid writes the entries of problems b, b + gridDim.x, ... (every block runs
+// the same per-key count and scan) and zeroes those problems' flag words; block 0 also the
+// header.  One block per problem of a batch: the fit's 24 x 512 schedule took 10.4 us on one
+// block (profiles/r05/r05t_prof_fit.txt), most of it one thread storing a key's tasks for
+// every problem in turn.
 __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, int batch,
                                                            int inv, int lead, int xd,
-                                                           int* zero, long long nzero,
+                                                           int* head, int nhead,
                                                            int* info, double* logdet,
                                                            int* flags, int fstride,
                                                            int preset_abort) {
   __shared__ int cnt[2][1024];
   const int T = threadIdx.x;
-  for (long long q = T; q < nzero; q += blockDim.x) zero[q] = 0;
-  for (int b = T; b < batch; b += blockDim.x) {
-    if (info) info[b] = 0;
-    if (logdet) logdet[b] = 0.0;
+  if (blockIdx.x == 0)
+    for (int q = T; q < nhead; q += blockDim.x) head[q] = 0;
+  for (int b = blockIdx.x; b < batch; b += gridDim.x) {
+    for (int q = T; q < fstride; q += blockDim.x) flags[(long long)b * fstride + q] = 0;
+    if (T == 0) {
+      if (info) info[b] = 0;
+      if (logdet) logdet[b] = 0.0;
+    }
   }
   const int nk = pp_nkeys(N, lead, xd);
   int own = 0;
@@ -1928,17 +1937,24 @@ __global__ __launch_bounds__(1024) void pp_schedule_kernel(int2* tasks, int N, i
     __syncthreads();
     src ^= 1;
   }
-  if (preset_abort)   // after the barriers above: the zeroing is complete
-    for (int b = T; b < batch; b += blockDim.x)
-      flags[(long long)b * fstride + 2 * N * N + 2 * N] = 2;
-  for (int b = T; b < batch; b += blockDim.x) tasks[b] = make_int2(kTChain | (b << 4), 0);
+  // (after the barriers above: this block's zeroing is complete)
+  if (T == 0)
+    for (int b = blockIdx.x; b < batch; b += gridDim.x) {
+      if (preset_abort) flags[(long long)b * fstride + 2 * N * N + 2 * N] = 2;
+      tasks[b] = make_int2(kTChain | (b << 4), 0);
+    }
   if (T >= nk) return;
   const int excl = cnt[src][T] - own;
   long long pos = batch + (long long)excl * batch;
   pp_for_key(T, N, inv != 0, lead, xd, [&](int kind, int i, int j) {
-    for (int b = 0; b < batch; ++b) tasks[pos++] = make_int2(kind | (b << 4), i | (j << 16));
+    for (int b = blockIdx.x; b < batch; b += gridDim.x)
+      tasks[pos + b] = make_int2(kind | (b << 4), i | (j << 16));
+    pos += batch;
   });
 }
+
+// Schedule blocks: one per problem up to one per CU (the rest loop)
+static int pp_schedule_grid(int batch) { return batch < 256 ? batch : 256; }
 
 // Tasks per problem, chain included (host side of the same enumeration; any lead gives the
 // same total).
@@ -2109,8 +2125,8 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   const int lead = pp_lead(batch, grid);
   const long long budget = g_poll_budget;
   // the schedule kernel also zeroes head + flags and info / logdet
-  hipLaunchKernelGGL(pp_schedule_kernel, dim3(1), dim3(1024), 0, stream, tasks, N, batch,
-                     inv ? 1 : 0, lead, kPPXDelay, head, (long long)(s.flag_bytes / sizeof(int)),
+  hipLaunchKernelGGL(pp_schedule_kernel, dim3(pp_schedule_grid(batch)), dim3(1024), 0, stream,
+                     tasks, N, batch, inv ? 1 : 0, lead, kPPXDelay, head, 256 / (int)sizeof(int),
                      info, logdet, flags, s.fstride, budget < 0 ? 1 : 0);
   GP_CK(hipGetLastError());
   if (pre.fn) {
