@@ -30,4 +30,14 @@ for s, e, n in ev:
     agg[k][0] += 1; agg[k][1] += e - s
 for k, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:15]:
     print(f"{k:60s} {c:7d} {t/1e6:9.1f} ms  {t/c/1e3:8.1f} us")
+# one Metropolis group in the middle of the run: kernels between consecutive pp_kernel starts
+pp = [i for i, (_, _, n) in enumerate(ev) if "pp_kernel" in n]
+if len(pp) > 10:
+    a, b = pp[len(pp) // 2], pp[len(pp) // 2 + 1]
+    base, prev_e = ev[a][0], None
+    print(f"one group ({(ev[b][0] - ev[a][0]) / 1e3:.1f} us pp_kernel start to start):")
+    for s, e, n in ev[a:b + 1]:
+        gap = (s - prev_e) / 1e3 if prev_e is not None else 0.0
+        print(f"  +{(s - base) / 1e3:8.1f} us  dur {(e - s) / 1e3:7.1f}  gap {gap:6.1f}  {key(n)}")
+        prev_e = e
 PY
