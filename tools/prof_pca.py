@@ -7,7 +7,10 @@ in a host timer bracketed by torch.cuda.synchronize(), and times each gp_dgemm c
 the ensemble with HIP events (achieved GB/s against 8 TB/s: bytes = the X operand read once +
 the small operands).  Prints one line per phase and a JSON summary.
 
-    python tools/prof_pca.py [ny] [n]
+    python tools/prof_pca.py [ny] [n] [--cold]
+
+--cold skips the small warm-up run, so first-use costs (HIP context, code-object loads, the
+caching allocator's first growth) land in the phases, as they do in bench.py --workload fit.
 """
 import json
 import os
@@ -24,8 +27,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from gladsgp_amd import blas, emulator, model as gmodel, svd as gsvd  # noqa: E402
 
-ny = int(sys.argv[1]) if len(sys.argv) > 1 else 1347945
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 512
+cold = "--cold" in sys.argv
+argv = [a for a in sys.argv[1:] if a != "--cold"]
+ny = int(argv[0]) if len(argv) > 0 else 1347945
+n = int(argv[1]) if len(argv) > 1 else 512
 dev = torch.device("cuda", 0)
 phases = defaultdict(float)
 gemms = []
@@ -87,8 +92,9 @@ tmp = tempfile.mkdtemp(prefix="gladsgp_pca_")
 try:
     np.random.seed(0)
     # warm-up at a small size (first-call HIP / library costs out of the timed run)
-    gmodel.init_model(t[:64], Y[:64, :4096], "warm", 8, data_dir=tmp, device=dev,
-                      recompute=True, verbose=False)
+    if not cold:
+        gmodel.init_model(t[:64], Y[:64, :4096], "warm", 8, data_dir=tmp, device=dev,
+                          recompute=True, verbose=False)
     phases.clear()
     gemms.clear()
     np.random.seed(0)
