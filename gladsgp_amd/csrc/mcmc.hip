@@ -26,6 +26,7 @@
 namespace {
 
 constexpr double kRhoMax = 0.999;   // rho clipped in the Beta prior (mcmc.RHO_MAX)
+constexpr int kLpTerms = 2048;      // log-posterior terms computed one per thread (LDS)
 
 struct GroupArgs {
   gp_mcmc_state S;
@@ -106,29 +107,35 @@ __global__ __launch_bounds__(1024) void mcmc_prep_kernel(GroupArgs A, double* __
   double* cand = S.scratch;                               // [i][P]
   double* okf = S.scratch + GPFIT_MCMC_MAX_GROUP * P;
   double* dlp = S.scratch + 2 * GPFIT_MCMC_MAX_GROUP * P;
-  if (A.flag && j < P) {                                  // betaU row 0: prior only
-    double *cur, step, up, ua;
-    update_refs(S, 0, j, cur, step, up, ua);
-    double c, dl;
-    bool ok;
-    propose(S, 0, *cur, step, up, c, ok, dl);
-    const bool acc = ok && (log(ua) < dl);
-    if (acc) *cur = c;
-    S.acc[j] += acc ? 1.0 : 0.0;
-  }
-  for (int i = 0; i < A.g; ++i) {
-    const int code = A.kinds[i];
-    const bool shared = code == d + 3;
-    if (j < (shared ? 1 : P)) {
+  // The prior-only move of betaU row 0 and the group's g proposals are independent (each reads
+  // the current state of its own element only; the Gram inputs below never read row 0), so
+  // thread t runs row 0's element t (t < P) or update t / P - 1's element t % P: one chain of
+  // fp64 exp / log per thread instead of up to g + 1 in turn (the kernel was 9.6-10.6 us,
+  // profiles/r05/r05_prof_fit2.txt).  The same arithmetic per element, so the same bits.
+  for (int t = j; t < (A.g + 1) * P; t += blockDim.x) {
+    const int i = t / P - 1, e = t - (t / P) * P;
+    if (i < 0) {                                          // betaU row 0: prior only
+      if (!A.flag) continue;
       double *cur, step, up, ua;
-      update_refs(S, code, j, cur, step, up, ua);
+      update_refs(S, 0, e, cur, step, up, ua);
       double c, dl;
       bool ok;
-      propose(S, param_of(code, d), *cur, step, up, c, ok, dl);
-      cand[i * P + j] = c;
-      okf[i * P + j] = ok ? 1.0 : 0.0;
-      dlp[i * P + j] = dl;
+      propose(S, 0, *cur, step, up, c, ok, dl);
+      const bool acc = ok && (log(ua) < dl);
+      if (acc) *cur = c;
+      S.acc[e] += acc ? 1.0 : 0.0;
+      continue;
     }
+    const int code = A.kinds[i];
+    if (code == d + 3 && e > 0) continue;                 // lamWOs: one element
+    double *cur, step, up, ua;
+    update_refs(S, code, e, cur, step, up, ua);
+    double c, dl;
+    bool ok;
+    propose(S, param_of(code, d), *cur, step, up, c, ok, dl);
+    cand[i * P + e] = c;
+    okf[i * P + e] = ok ? 1.0 : 0.0;
+    dlp[i * P + e] = dl;
   }
   __syncthreads();
   if (j >= P) return;
@@ -201,8 +208,24 @@ __global__ __launch_bounds__(1024) void mcmc_decide_kernel(GroupArgs A,
     __syncthreads();
   }
   if (!A.flag) return;
-  // log posterior of the state reached (mcmc.GPUSampler.log_post)
-  if (j < P) {
+  // log posterior of the state reached (mcmc.GPUSampler.log_post).  The d + 3 prior terms of
+  // each GP are independent: with room in LDS one thread per term, then thread j adds its GP's
+  // terms in the serial order (same bits; d + 3 fp64 log / exp chains in turn before)
+  __shared__ double terms[kLpTerms];
+  const int nt = (d + 3) * P;
+  if (nt <= kLpTerms) {
+    for (int t = j; t < nt; t += blockDim.x) {
+      const int q = t / P, e = t - q * P;
+      terms[t] = q <= d ? log_prior(S, 0, S.betaU[(long long)q * P + e])
+                        : (q == d + 1 ? log_prior(S, 1, S.lamUz[e]) : log_prior(S, 2, S.lamWs[e]));
+    }
+    __syncthreads();
+    if (j < P) {
+      double t = S.ll[j];
+      for (int q = 0; q < d + 3; ++q) t += terms[q * P + j];
+      sh[j] = t;
+    }
+  } else if (j < P) {
     double t = S.ll[j];
     for (int r = 0; r <= d; ++r) t += log_prior(S, 0, S.betaU[(long long)r * P + j]);
     t += log_prior(S, 1, S.lamUz[j]);
