@@ -91,6 +91,9 @@ SIGNATURES = {
     "gp_mcmc_group_prep": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
     "gp_mcmc_group_decide": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "gp_mcmc_group_step": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
     "gp_realize": (c_int, [c_void_p, c_void_p, c_ll, ctypes.c_ulonglong, ctypes.c_ulonglong,
                            c_void_p, c_void_p]),
     "gp_dgemm_ws_bytes": (c_ll, [c_int, c_int, c_int]),

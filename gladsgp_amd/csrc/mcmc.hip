@@ -14,6 +14,7 @@
 //   gp_mcmc_group_decide  the accept / reject decisions in order (per GP; lamWOs once for all
 //                         on the sum), state, per-GP likelihood and acceptance counters in place,
 //                         and for the sweep's last group the log posterior
+//   gp_mcmc_group_step    one group's decide and the next group's prep in one launch
 // They replace some 100 elementwise launches per group of the tensor-op form of the same sweep
 // (mcmc.py _sweep_torch, kept as the host-logic reference the CPU tests run).  Arithmetic is
 // op-for-op that form's (no FMA contraction), so the chains agree with it and with the oracle
@@ -99,9 +100,8 @@ GP_DEV void propose(const gp_mcmc_state& S, int p, double x, double step, double
   dlp = log_prior(S, p, cand) - log_prior(S, p, x);
 }
 
-__global__ __launch_bounds__(1024) void mcmc_prep_kernel(GroupArgs A, double* __restrict__ beta,
-                                                         double* __restrict__ s,
-                                                         double* __restrict__ delta) {
+GP_DEV void prep_body(const GroupArgs& A, double* __restrict__ beta, double* __restrict__ s,
+                      double* __restrict__ delta) {
   const gp_mcmc_state& S = A.S;
   const int j = threadIdx.x, P = S.P, d = S.d;
   double* cand = S.scratch;                               // [i][P]
@@ -164,8 +164,7 @@ __global__ __launch_bounds__(1024) void mcmc_prep_kernel(GroupArgs A, double* __
   }
 }
 
-__global__ __launch_bounds__(1024) void mcmc_decide_kernel(GroupArgs A,
-                                                           const double* __restrict__ ll_all) {
+GP_DEV void decide_body(const GroupArgs& A, const double* __restrict__ ll_all) {
   const gp_mcmc_state& S = A.S;
   const int j = threadIdx.x, P = S.P, d = S.d;
   const double* cand = S.scratch;
@@ -240,6 +239,29 @@ __global__ __launch_bounds__(1024) void mcmc_decide_kernel(GroupArgs A,
   }
 }
 
+__global__ __launch_bounds__(1024) void mcmc_prep_kernel(GroupArgs A, double* __restrict__ beta,
+                                                         double* __restrict__ s,
+                                                         double* __restrict__ delta) {
+  prep_body(A, beta, s, delta);
+}
+
+__global__ __launch_bounds__(1024) void mcmc_decide_kernel(GroupArgs A,
+                                                           const double* __restrict__ ll_all) {
+  decide_body(A, ll_all);
+}
+
+// A group's decisions, then the next group's proposals and Gram inputs, in one launch (the
+// barrier orders the decisions' state and scratch reads before the proposals' writes)
+__global__ __launch_bounds__(1024) void mcmc_step_kernel(GroupArgs D,
+                                                         const double* __restrict__ ll_all,
+                                                         GroupArgs A, double* __restrict__ beta,
+                                                         double* __restrict__ s,
+                                                         double* __restrict__ delta) {
+  decide_body(D, ll_all);
+  __syncthreads();
+  prep_body(A, beta, s, delta);
+}
+
 int group_args(const gp_mcmc_state* S, const int* kinds, int g, int flag, GroupArgs& A) {
   if (!S) return -1;
   if (S->P < 1 || S->P > 1024) return -2;
@@ -272,6 +294,24 @@ extern "C" int gp_mcmc_group_prep(const gp_mcmc_state* S, const int* kinds, int 
   if (!beta || !s || !delta) return -7;
   hipLaunchKernelGGL(mcmc_prep_kernel, dim3(1), dim3(block_for(S->P)), 0, stream, A, beta, s,
                      delta);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+extern "C" int gp_mcmc_group_step(const gp_mcmc_state* S, const int* kinds, int g, int last,
+                                  const double* ll_all, const gp_mcmc_state* S_next,
+                                  const int* kinds_next, int g_next, int first, double* beta,
+                                  double* s, double* delta, hipStream_t stream) {
+  GroupArgs D, A;
+  int rc = group_args(S, kinds, g, last, D);
+  if (rc) return rc;
+  if (!ll_all) return -7;
+  rc = group_args(S_next, kinds_next, g_next, first, A);
+  if (rc) return rc - 10;
+  if (!beta || !s || !delta) return -17;
+  if (S_next->P != S->P) return -18;
+  hipLaunchKernelGGL(mcmc_step_kernel, dim3(1), dim3(block_for(S->P)), 0, stream, D, ll_all, A,
+                     beta, s, delta);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }

@@ -234,6 +234,8 @@ class GPUSampler:
         self.graph = None
         # sweeps per replayed graph in run() (GPFIT_MCMC_BLOCK; 1: one sweep per replay)
         self.block = max(1, int(os.environ.get("GPFIT_MCMC_BLOCK", "16")))
+        # decide + next prep in one launch (gp_mcmc_group_step); GPFIT_MCMC_MERGE=0: two
+        self._merge = os.environ.get("GPFIT_MCMC_MERGE", "1") == "1"
         self._bgraph = {}
         self.st = None
         if spec is None:
@@ -417,22 +419,38 @@ class GPUSampler:
 
     def _sweep_fused(self) -> None:
         """The sweep of _sweep_torch with each speculative group's proposals and decisions in
-        two single-workgroup kernels around its gp_loglik (gp_mcmc_group_prep / _decide,
-        csrc/mcmc.hip): 3 launches + gp_loglik's per group instead of ~100."""
+        single-workgroup kernels around its gp_loglik (csrc/mcmc.hip): the first group's
+        gp_mcmc_group_prep, then after each gp_loglik one gp_mcmc_group_step (this group's
+        decisions + the next group's proposals; gp_mcmc_group_decide after the last), so
+        2 + gp_loglik's launches per group instead of ~100."""
         self._S = self._state_struct()          # kept alive: the library reads it per call
+        S = ctypes.addressof(self._S)
         stream = kernels._stream(self.dev)
         last = len(self.groups) - 1
+        kinds = [(ctypes.c_int * len(g))(*[self._code(u) for u in g]) for g in self.groups]
+        self._kinds = kinds                     # (kept alive with _S)
+        bufs = [self._gbuf[2 ** len(g) - 1] for g in self.groups]
+        b0 = bufs[0]
+        _capi.call("gp_mcmc_group_prep", S, ctypes.addressof(kinds[0]), len(self.groups[0]), 1,
+                   b0["beta"].data_ptr(), b0["s"].data_ptr(), b0["delta"].data_ptr(), stream)
         for gi, grp in enumerate(self.groups):
-            buf = self._gbuf[2 ** len(grp) - 1]
-            kinds = (ctypes.c_int * len(grp))(*[self._code(g) for g in grp])
-            _capi.call("gp_mcmc_group_prep", ctypes.addressof(self._S), ctypes.addressof(kinds),
-                       len(grp), int(gi == 0), buf["beta"].data_ptr(), buf["s"].data_ptr(),
-                       buf["delta"].data_ptr(), stream)
+            buf = bufs[gi]
             kernels.loglik(self.X, buf["beta"], buf["s"], buf["delta"], buf["w"], buf["ws"],
                            out=buf["ll"])
-            _capi.call("gp_mcmc_group_decide", ctypes.addressof(self._S),
-                       ctypes.addressof(kinds), len(grp), int(gi == last), buf["ll"].data_ptr(),
-                       stream)
+            if gi == last or not self._merge:
+                _capi.call("gp_mcmc_group_decide", S, ctypes.addressof(kinds[gi]), len(grp),
+                           int(gi == last), buf["ll"].data_ptr(), stream)
+                if gi < last:
+                    nb = bufs[gi + 1]
+                    _capi.call("gp_mcmc_group_prep", S, ctypes.addressof(kinds[gi + 1]),
+                               len(self.groups[gi + 1]), 0, nb["beta"].data_ptr(),
+                               nb["s"].data_ptr(), nb["delta"].data_ptr(), stream)
+            else:
+                nb = bufs[gi + 1]
+                _capi.call("gp_mcmc_group_step", S, ctypes.addressof(kinds[gi]), len(grp), 0,
+                           buf["ll"].data_ptr(), S, ctypes.addressof(kinds[gi + 1]),
+                           len(self.groups[gi + 1]), 0, nb["beta"].data_ptr(),
+                           nb["s"].data_ptr(), nb["delta"].data_ptr(), stream)
 
     def _sweep_torch(self) -> None:
         """One component-wise Metropolis sweep on the static buffers (graph-capturable: no

@@ -319,7 +319,13 @@ int gp_loglik_status(void* ws, int n, int batch, int reset, hipStream_t stream);
  *                        (x d), s and delta: the batch for gp_loglik;
  *   gp_mcmc_group_decide takes the decisions in order from gp_loglik's ll_all (per GP; lamWOs
  *                        once on the sum), updates state, ll and counters in place and
- *                        (last != 0) writes the log posterior to lp.
+ *                        (last != 0) writes the log posterior to lp;
+ *   gp_mcmc_group_step   gp_mcmc_group_decide of one group (S, kinds, g, last, ll_all) then
+ *                        gp_mcmc_group_prep of the next (S_next, kinds_next, g_next, first,
+ *                        beta, s, delta) in one launch (one kernel boundary less per group);
+ *                        the same results as the two calls in turn.  Argument errors of the
+ *                        second group are its prep's codes - 10; S_next->P must equal S->P
+ *                        (-18).
  * Single-workgroup launches (P <= 1024), stream-ordered, graph-capturable; 0 or < 0 (argument).
  */
 #define GPFIT_MCMC_MAX_GROUP 4
@@ -353,6 +359,10 @@ int gp_mcmc_group_prep(const gp_mcmc_state* S, const int* kinds, int g, int firs
                        double* beta, double* s, double* delta, hipStream_t stream);
 int gp_mcmc_group_decide(const gp_mcmc_state* S, const int* kinds, int g, int last,
                          const double* ll_all, hipStream_t stream);
+int gp_mcmc_group_step(const gp_mcmc_state* S, const int* kinds, int g, int last,
+                       const double* ll_all, const gp_mcmc_state* S_next, const int* kinds_next,
+                       int g_next, int first, double* beta, double* s, double* delta,
+                       hipStream_t stream);
 
 /*
  * Host-side (no device, no stream): `count` float32 deviates of numpy's legacy global

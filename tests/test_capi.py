@@ -150,6 +150,35 @@ def test_new_entry_points_validate(lib):
     assert lib.gp_ctx_set_aux_chunks(dummy, -5) == -2      # rejected before the handle is read
 
 
+def test_mcmc_group_step_validates(lib):
+    """gp_mcmc_group_step: both groups' arguments are checked before the launch (the second
+    group's prep codes shifted by -10)."""
+    from gladsgp_amd import _capi
+    S = _capi.McmcState()
+    for nm, _ in S._fields_[:14]:
+        setattr(S, nm, 64)                           # non-null, never dereferenced here
+    S.P, S.d = 4, 2
+    T = _capi.McmcState()
+    ctypes.pointer(T)[0] = S
+    k = (ctypes.c_int * 2)(1, 2)
+    dummy = ctypes.c_void_p(64)
+    pS, pT = ctypes.addressof(S), ctypes.addressof(T)
+    assert lib.gp_mcmc_group_step(None, k, 2, 0, dummy, pT, k, 2, 0, dummy, dummy, dummy,
+                                  None) == -1
+    assert lib.gp_mcmc_group_step(pS, k, 2, 0, None, pT, k, 2, 0, dummy, dummy, dummy,
+                                  None) == -7
+    assert lib.gp_mcmc_group_step(pS, k, 2, 0, dummy, None, k, 2, 0, dummy, dummy, dummy,
+                                  None) == -11
+    bad = (ctypes.c_int * 2)(1, 9)                   # update code > d + 3
+    assert lib.gp_mcmc_group_step(pS, k, 2, 0, dummy, pT, bad, 2, 0, dummy, dummy, dummy,
+                                  None) == -16
+    assert lib.gp_mcmc_group_step(pS, k, 2, 0, dummy, pT, k, 2, 0, None, dummy, dummy,
+                                  None) == -17
+    T.P = 5
+    assert lib.gp_mcmc_group_step(pS, k, 2, 0, dummy, pT, k, 2, 0, dummy, dummy, dummy,
+                                  None) == -18
+
+
 def test_comm_argument_validation(lib):
     # RCCL wrappers: bad arguments are rejected before librccl is touched
     dummy = ctypes.c_void_p(16)

@@ -203,3 +203,22 @@ def test_block_graph_equals_eager(dev, block):
         np.testing.assert_array_equal(recs[1][k], recs[0][k], err_msg=k)
     for k in cnts[0]:
         np.testing.assert_array_equal(cnts[1][k], cnts[0][k], err_msg=str(k))
+
+
+def test_merged_group_step_equals_two_launches(dev, monkeypatch):
+    """gp_mcmc_group_step (a group's decisions + the next group's proposals in one launch)
+    gives the chain, records and counters of gp_mcmc_group_decide + gp_mcmc_group_prep."""
+    n, d, P = 64, 3, 4
+    X, w, lam = _problem(n, d, P, seed=61)
+    recs, cnts = [], []
+    for merge in ("0", "1"):
+        monkeypatch.setenv("GPFIT_MCMC_MERGE", merge)
+        pr = mcmc.ModelParams(d, P)
+        sampler = mcmc.GPUSampler(_t(X, dev), _t(w, dev), _t(lam, dev), pr, spec=2)
+        assert sampler._merge == (merge == "1")
+        recs.append(sampler.run(21, np.random.default_rng(23)))
+        cnts.append(sampler.counts())
+    for k in ("betaU", "lamUz", "lamWs", "lamWOs", "logPost"):
+        np.testing.assert_array_equal(recs[1][k], recs[0][k], err_msg=k)
+    for k in cnts[0]:
+        np.testing.assert_array_equal(cnts[1][k], cnts[0][k], err_msg=str(k))
