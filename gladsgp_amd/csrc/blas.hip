@@ -465,38 +465,66 @@ __global__ __launch_bounds__(256, TSM_OCC) void gemm_tsm_kernel(int M, int N, in
     pcol[t] = P + (rok[t] ? r : 0);
   }
   const int jc0 = li, jc1 = 16 + li;
-  // K-group of 16: lane (row li, slot ks) holds k = k0 + 4u + ks of its 4 row tiles
+  // K-group of 16: lane (row li, slot ks) holds k = k0 + 4u + ks of its 4 row tiles.
+  // FULL (every block row < M and K % 16 == 0, i.e. all but a product's last block): no
+  // per-load masks and one 64-bit address per (group, u) -- the masked form's per-load
+  // exec-mask branches and 64-bit multiplies outnumbered its MFMAs (r05_pmc_ts.txt: MFMA busy
+  // 0.46 with waves waiting only 19% of their cycles).  Columns >= N then multiply a clamped,
+  // finite column of Q into C columns that are never stored; every stored element sums the
+  // same products in the same order, so the results are the masked form's bits.
+  const int jc1c = jc1 < N ? jc1 : N - 1;
+  const long long ldp4 = 4LL * ldp, qk4 = 4LL * qk;
+  const EQ* const qc0 = Q + jc0 * qj;
+  const EQ* const qc1 = Q + jc1c * qj;
   double a[kTsRing][T][4], bv[kTsRing][4][2];
-  auto load = [&](double (&ab)[T][4], double (&bb)[4][2], int k0) {
+  auto run = [&](auto fullc) {
+    constexpr bool FULL = decltype(fullc)::value;
+    auto load = [&](double (&ab)[T][4], double (&bb)[4][2], int k0) {
+      if constexpr (FULL) {
+        const EP* pk = P + rbase + li + (long long)(k0 + ks) * ldp;
+        const long long qo = (long long)(k0 + ks) * qk;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k0 + 4 * u + ks;
-      const bool kok = k < K;
+        for (int u = 0; u < 4; ++u) {
+          const EP* pu = pk + u * ldp4;
 #pragma unroll
-      for (int t = 0; t < T; ++t)
-        ab[t][u] = (kok && rok[t]) ? static_cast<double>(pcol[t][(long long)k * ldp]) : 0.0;
-      bb[u][0] = (kok && jc0 < N) ? static_cast<double>(Q[k * qk + jc0 * qj]) : 0.0;
-      bb[u][1] = (kok && jc1 < N) ? static_cast<double>(Q[k * qk + jc1 * qj]) : 0.0;
+          for (int t = 0; t < T; ++t) ab[t][u] = static_cast<double>(pu[16 * t]);
+          bb[u][0] = static_cast<double>(qc0[qo + u * qk4]);
+          bb[u][1] = static_cast<double>(qc1[qo + u * qk4]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + 4 * u + ks;
+          const bool kok = k < K;
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+            ab[t][u] = (kok && rok[t]) ? static_cast<double>(pcol[t][(long long)k * ldp]) : 0.0;
+          bb[u][0] = (kok && jc0 < N) ? static_cast<double>(Q[k * qk + jc0 * qj]) : 0.0;
+          bb[u][1] = (kok && jc1 < N) ? static_cast<double>(Q[k * qk + jc1 * qj]) : 0.0;
+        }
+      }
+    };
+#pragma unroll
+    for (int q = 0; q < kTsRing - 1; ++q) load(a[q], bv[q], 16 * q);
+    for (int k0 = 0; k0 < K; k0 += 16 * kTsRing) {
+#pragma unroll
+      for (int q = 0; q < kTsRing; ++q) {
+        const int kq = k0 + 16 * q;
+        if (kq >= K) break;
+        const int kn = kq + 16 * (kTsRing - 1);
+        if (kn < K) load(a[(q + kTsRing - 1) % kTsRing], bv[(q + kTsRing - 1) % kTsRing], kn);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int t = 0; t < T; ++t) {
+            acc[t][0] = mfma16x16x4(a[q][t][u], bv[q][u][0], acc[t][0]);
+            acc[t][1] = mfma16x16x4(a[q][t][u], bv[q][u][1], acc[t][1]);
+          }
+      }
     }
   };
-#pragma unroll
-  for (int q = 0; q < kTsRing - 1; ++q) load(a[q], bv[q], 16 * q);
-  for (int k0 = 0; k0 < K; k0 += 16 * kTsRing) {
-#pragma unroll
-    for (int q = 0; q < kTsRing; ++q) {
-      const int kq = k0 + 16 * q;
-      if (kq >= K) break;
-      const int kn = kq + 16 * (kTsRing - 1);
-      if (kn < K) load(a[(q + kTsRing - 1) % kTsRing], bv[(q + kTsRing - 1) % kTsRing], kn);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          acc[t][0] = mfma16x16x4(a[q][t][u], bv[q][u][0], acc[t][0]);
-          acc[t][1] = mfma16x16x4(a[q][t][u], bv[q][u][1], acc[t][1]);
-        }
-    }
-  }
+  if (i0 + kTsmRows <= M && K % 16 == 0) run(std::true_type{});
+  else run(std::false_type{});
 #pragma unroll
   for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -550,58 +578,87 @@ __global__ __launch_bounds__(64 * kTskWaves, 8 / kTskWaves) void gemm_tsk16_kern
   const double* lrow = P + (long long)(row0 + rr) * ldp + 2 * c;
   const long long qstep = 8LL * ldp;
   const int jc0 = li, jc1 = 16 + li;
+  // FULL (the block's rows < M and its k range whole groups of 16: all but a product's last
+  // slice): loads without per-lane masks and one 64-bit multiply per W group, as in tsm
+  // (the masked form spent more instructions on exec-mask branches and 64-bit address
+  // arithmetic than on MFMAs: profiles/r05/r05_pmc_ts.txt, MFMA busy 0.49).  Columns >= N
+  // read a clamped, finite column of W into C columns that are never stored: same bits.
+  const int jc1c = jc1 < N ? jc1 : N - 1;
+  const EW* const wc0 = W + jc0 * wj;
+  const EW* const wc1 = W + jc1c * wj;
+  const long long wk4 = 4LL * wk;
   double2 xr[RX][8];
   double bv[RW][4][2];
-  // (k0 + 2c even < ke: the pair's second element is inside the padded row; zeroed past ke)
-  auto load_x = [&](double2 (&xb)[8], int k0) {
-    const int k = k0 + 2 * c;
+  auto run = [&](auto fullc) {
+    constexpr bool FULL = decltype(fullc)::value;
+    // (k0 + 2c even < ke: the pair's second element is inside the padded row; zeroed past ke)
+    auto load_x = [&](double2 (&xb)[8], int k0) {
+      if constexpr (FULL) {
+        const double* lk = lrow + k0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      double2 v = make_double2(0.0, 0.0);
-      if (k < ke && row0 + 8 * q + rr < M)
-        v = *reinterpret_cast<const double2*>(lrow + q * qstep + k0);
-      if (k + 1 >= ke) v.y = 0.0;
-      xb[q] = v;
-    }
-  };
-  auto load_w = [&](double (&bb)[4][2], int k0) {
+        for (int q = 0; q < 8; ++q) xb[q] = *reinterpret_cast<const double2*>(lk + q * qstep);
+      } else {
+        const int k = k0 + 2 * c;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k0 + 4 * u + ks;
-      const bool ok = k < ke;
-      bb[u][0] = (ok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
-      bb[u][1] = (ok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
-    }
-  };
-  load_x(xr[0], kb);
-  load_w(bv[0], kb);
-  load_x(xr[1], kb + G);
-  for (int k0 = kb; k0 < ke; k0 += G * RX * RW) {
-    static_for<0, RX * RW, 1>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      const int kq = k0 + G * q;
-      if (kq >= ke) return;
-      if (kq + 2 * G < ke) load_x(xr[(q + 2) % RX], kq + 2 * G);
-      if (kq + G < ke) load_w(bv[(q + 1) % RW], kq + G);
-      // transpose: xw[k][row] (one wave's LDS: its own DS instructions run in order)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        xw[(2 * c) * kTsk16Pitch + 8 * i + rr] = xr[q % RX][i].x;
-        xw[(2 * c + 1) * kTsk16Pitch + 8 * i + rr] = xr[q % RX][i].y;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        double a[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) a[t] = xw[(4 * u + ks) * kTsk16Pitch + 16 * t + li];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          acc[t][0] = mfma16x16x4(a[t], bv[q % RW][u][0], acc[t][0]);
-          acc[t][1] = mfma16x16x4(a[t], bv[q % RW][u][1], acc[t][1]);
+        for (int q = 0; q < 8; ++q) {
+          double2 v = make_double2(0.0, 0.0);
+          if (k < ke && row0 + 8 * q + rr < M)
+            v = *reinterpret_cast<const double2*>(lrow + q * qstep + k0);
+          if (k + 1 >= ke) v.y = 0.0;
+          xb[q] = v;
         }
       }
-    });
-  }
+    };
+    auto load_w = [&](double (&bb)[4][2], int k0) {
+      if constexpr (FULL) {
+        const long long wo = (long long)(k0 + ks) * wk;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          bb[u][0] = static_cast<double>(wc0[wo + u * wk4]);
+          bb[u][1] = static_cast<double>(wc1[wo + u * wk4]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + 4 * u + ks;
+          const bool ok = k < ke;
+          bb[u][0] = (ok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
+          bb[u][1] = (ok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
+        }
+      }
+    };
+    load_x(xr[0], kb);
+    load_w(bv[0], kb);
+    load_x(xr[1], kb + G);
+    for (int k0 = kb; k0 < ke; k0 += G * RX * RW) {
+      static_for<0, RX * RW, 1>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const int kq = k0 + G * q;
+        if (kq >= ke) return;
+        if (kq + 2 * G < ke) load_x(xr[(q + 2) % RX], kq + 2 * G);
+        if (kq + G < ke) load_w(bv[(q + 1) % RW], kq + G);
+        // transpose: xw[k][row] (one wave's LDS: its own DS instructions run in order)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xw[(2 * c) * kTsk16Pitch + 8 * i + rr] = xr[q % RX][i].x;
+          xw[(2 * c + 1) * kTsk16Pitch + 8 * i + rr] = xr[q % RX][i].y;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          double a[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) a[t] = xw[(4 * u + ks) * kTsk16Pitch + 16 * t + li];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            acc[t][0] = mfma16x16x4(a[t], bv[q % RW][u][0], acc[t][0]);
+            acc[t][1] = mfma16x16x4(a[t], bv[q % RW][u][1], acc[t][1]);
+          }
+        }
+      });
+    }
+  };
+  if (rg * kTskRows + kTskRows <= M && (ke - kb) % G == 0) run(std::true_type{});
+  else run(std::false_type{});
   double* pp = part + (long long)slice * M * N;
 #pragma unroll
   for (int t = 0; t < 4; ++t)

@@ -196,17 +196,20 @@ def randomized_svd(X, p, k=None, q=1, return_error=False, omega=None, device=Non
         omega = legacy_normal_f32((n_cols, r))
     Om = _to_device(omega, dev).contiguous()      # float32 (as drawn) or float64
     Xc = CM.of_rowmajor(Xt)          # (n_cols x m_rows), ld = n_cols
-    # Omega widened to fp64 (exactly) and column-major (n_cols x r, ld = n_cols) in one copy:
-    # the tall-skinny X Omega with a float32 W ran 2.15-2.51 ms against 1.31-1.47 with an fp64
-    # one at the fit's shape (profiles/r05/r05k_ts_probe.log, r05l_prof_pca.log).  The kernel
-    # widens a float32 operand exactly on load, so the sums are the same bits either way.
-    Ow = torch.empty((r, n_cols), dtype=torch.float64, device=Om.device)
-    Ow.copy_(Om.t())
-    Oc = CM(Ow, n_cols, r, max(n_cols, 1))
-    Y = gemm(True, False, Xc, Oc)    # (m_rows x r) = X Omega
+    # Omega as drawn (float32, row-major n_cols x r = column-major r x n_cols, ld = r), read
+    # in place and widened exactly on load: with the tall-skinny kernels' unmasked fast path
+    # X Omega runs 1.13 ms against 1.23 for an fp64 column-major copy of Omega (which the
+    # masked kernel needed: 2.1 vs 1.3-1.5 ms, profiles/r05/r05k_ts_probe.log), and the copy
+    # itself is gone (profiles/r05/r05_tsfast_ab.log).  Same sums, same bits.
+    Oc = CM.of_rowmajor(Om)          # (r x n_cols)
+    Y = gemm(True, True, Xc, Oc)     # (m_rows x r) = X Omega
     for _ in range(q):
-        Z = gemm(False, False, Xc, Y)    # (n_cols x r) = X^T Y
-        Y = gemm(True, False, Xc, Z)     # (m_rows x r) = X X^T Y
+        # Z = X^T Y made as Z^T = Y^T X (r x n_cols: the same products in the same order, laid
+        # out row-major), so X Z reads Z's r values of each k contiguously, as X Omega reads
+        # Omega (profiles/r05/r05_tsfast2_pca.log: X Z with a column-major Z was the slowest
+        # of the four ensemble-streaming products)
+        Zt = gemm(True, True, Y, Xc)     # (r x n_cols) = Y^T X = (X^T Y)^T
+        Y = gemm(True, True, Xc, Zt)     # (m_rows x r) = X X^T Y
     if r > m_rows:
         # more test vectors than rows: range(Y) is all of R^m_rows (numpy's reduced QR gives
         # an m_rows x m_rows Q), so keep m_rows of them
