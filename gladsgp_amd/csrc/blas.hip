@@ -384,45 +384,68 @@ __global__ __launch_bounds__(64 * kTskWaves, 8 / kTskWaves) void gemm_tsk_kernel
   const EP* lrow = P + (long long)(row0 + rr) * ldp + kk;
   const long long qstep = (long long)RS * ldp;
   const int jc0 = li, jc1 = 16 + li;
+  // FULL: the unmasked fast path of tsk16 / tsm (rows < M, whole groups; same bits)
+  const int jc0c = jc0 < N ? jc0 : N - 1, jc1c = jc1 < N ? jc1 : N - 1;   // N < 16 too
+  const EW* const wc0 = W + jc0c * wj;
+  const EW* const wc1 = W + jc1c * wj;
+  const long long wk4 = 4LL * wk;
   double xr[R][NQ], bv[R][G / 4][2];
-  auto load = [&](double (&xb)[NQ], double (&bb)[G / 4][2], int k0) {
-    const bool kok = k0 + kk < ke;
+  auto run = [&](auto fullc) {
+    constexpr bool FULL = decltype(fullc)::value;
+    auto load = [&](double (&xb)[NQ], double (&bb)[G / 4][2], int k0) {
+      if constexpr (FULL) {
+        const EP* lk = lrow + k0;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      xb[q] = (kok && row0 + RS * q + rr < M) ? static_cast<double>(lrow[q * qstep + k0]) : 0.0;
+        for (int q = 0; q < NQ; ++q) xb[q] = static_cast<double>(lk[q * qstep]);
+        const long long wo = (long long)(k0 + ks) * wk;
 #pragma unroll
-    for (int u = 0; u < G / 4; ++u) {
-      const int k = k0 + 4 * u + ks;
-      const bool ok = k < ke;
-      bb[u][0] = (ok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
-      bb[u][1] = (ok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
-    }
-  };
+        for (int u = 0; u < G / 4; ++u) {
+          bb[u][0] = static_cast<double>(wc0[wo + u * wk4]);
+          bb[u][1] = static_cast<double>(wc1[wo + u * wk4]);
+        }
+      } else {
+        const bool kok = k0 + kk < ke;
 #pragma unroll
-  for (int q = 0; q < R - 1; ++q) load(xr[q], bv[q], kb + G * q);
-  for (int k0 = kb; k0 < ke; k0 += G * R) {
+        for (int q = 0; q < NQ; ++q)
+          xb[q] = (kok && row0 + RS * q + rr < M) ? static_cast<double>(lrow[q * qstep + k0])
+                                                   : 0.0;
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-      const int kq = k0 + G * q;
-      if (kq >= ke) break;
-      const int kn = kq + G * (R - 1);                    // the group R - 1 ahead
-      if (kn < ke) load(xr[(q + R - 1) % R], bv[(q + R - 1) % R], kn);
-      // transpose: xw[k][row] (one wave's LDS: its own DS instructions run in order)
+        for (int u = 0; u < G / 4; ++u) {
+          const int k = k0 + 4 * u + ks;
+          const bool ok = k < ke;
+          bb[u][0] = (ok && jc0 < N) ? static_cast<double>(W[k * wk + jc0 * wj]) : 0.0;
+          bb[u][1] = (ok && jc1 < N) ? static_cast<double>(W[k * wk + jc1 * wj]) : 0.0;
+        }
+      }
+    };
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) xw[kk * kTskPitch + RS * i + rr] = xr[q][i];
+    for (int q = 0; q < R - 1; ++q) load(xr[q], bv[q], kb + G * q);
+    for (int k0 = kb; k0 < ke; k0 += G * R) {
 #pragma unroll
-      for (int u = 0; u < G / 4; ++u) {
-        double a[4];
+      for (int q = 0; q < R; ++q) {
+        const int kq = k0 + G * q;
+        if (kq >= ke) break;
+        const int kn = kq + G * (R - 1);                    // the group R - 1 ahead
+        if (kn < ke) load(xr[(q + R - 1) % R], bv[(q + R - 1) % R], kn);
+        // transpose: xw[k][row] (one wave's LDS: its own DS instructions run in order)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) a[t] = xw[(4 * u + ks) * kTskPitch + 16 * t + li];
+        for (int i = 0; i < NQ; ++i) xw[kk * kTskPitch + RS * i + rr] = xr[q][i];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          acc[t][0] = mfma16x16x4(a[t], bv[q][u][0], acc[t][0]);
-          acc[t][1] = mfma16x16x4(a[t], bv[q][u][1], acc[t][1]);
+        for (int u = 0; u < G / 4; ++u) {
+          double a[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) a[t] = xw[(4 * u + ks) * kTskPitch + 16 * t + li];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            acc[t][0] = mfma16x16x4(a[t], bv[q][u][0], acc[t][0]);
+            acc[t][1] = mfma16x16x4(a[t], bv[q][u][1], acc[t][1]);
+          }
         }
       }
     }
-  }
+  };
+  if (rg * kTskRows + kTskRows <= M && (ke - kb) % G == 0) run(std::true_type{});
+  else run(std::false_type{});
   // C layout: lane l, reg q holds C[(l >> 4) + 4q][l & 15] of each 16 x 16 tile
   double* pp = part + (long long)slice * M * N;
 #pragma unroll
@@ -472,9 +495,9 @@ __global__ __launch_bounds__(256, TSM_OCC) void gemm_tsm_kernel(int M, int N, in
   // 0.46 with waves waiting only 19% of their cycles).  Columns >= N then multiply a clamped,
   // finite column of Q into C columns that are never stored; every stored element sums the
   // same products in the same order, so the results are the masked form's bits.
-  const int jc1c = jc1 < N ? jc1 : N - 1;
+  const int jc0c = jc0 < N ? jc0 : N - 1, jc1c = jc1 < N ? jc1 : N - 1;   // N < 16 too
   const long long ldp4 = 4LL * ldp, qk4 = 4LL * qk;
-  const EQ* const qc0 = Q + jc0 * qj;
+  const EQ* const qc0 = Q + jc0c * qj;
   const EQ* const qc1 = Q + jc1c * qj;
   double a[kTsRing][T][4], bv[kTsRing][4][2];
   auto run = [&](auto fullc) {
@@ -583,8 +606,8 @@ __global__ __launch_bounds__(64 * kTskWaves, 8 / kTskWaves) void gemm_tsk16_kern
   // (the masked form spent more instructions on exec-mask branches and 64-bit address
   // arithmetic than on MFMAs: profiles/r05/r05_pmc_ts.txt, MFMA busy 0.49).  Columns >= N
   // read a clamped, finite column of W into C columns that are never stored: same bits.
-  const int jc1c = jc1 < N ? jc1 : N - 1;
-  const EW* const wc0 = W + jc0 * wj;
+  const int jc0c = jc0 < N ? jc0 : N - 1, jc1c = jc1 < N ? jc1 : N - 1;   // N < 16 too
+  const EW* const wc0 = W + jc0c * wj;
   const EW* const wc1 = W + jc1c * wj;
   const long long wk4 = 4LL * wk;
   double2 xr[RX][8];
