@@ -332,7 +332,7 @@ def main():
                     help="c3: CUs the cross-covariance stream leaves free (-1: library default)")
     ap.add_argument("--aux-chunks", type=int, default=None,
                     help="gp_ctx_set_aux_chunks: chunks whose cross-covariance runs on the aux "
-                         "stream (-1: all; default: all for c3, 4 for c4)")
+                         "stream (-1: all; default: all for c3, 1 for c4)")
     ap.add_argument("--pcs", type=int, default=32, help="c4: number of PC GPs")
     ap.add_argument("--c4-path", choices=("fit_predict", "predict"), default="fit_predict",
                     help="c4: one gp_fit_predict per step with the first --aux-chunks chunks' "
@@ -587,8 +587,10 @@ def main_c4(args):
     ws = kernels.PredictWorkspace()
     mean = torch.empty((bl, m), dtype=torch.float64, device=dev)
     var = torch.empty((bl, m), dtype=torch.float64, device=dev)
-    # 4: 52.93-52.98 vs 52.39-52.87 M/s for 2 on one box (profiles/r04/r04j_c4aux.log)
-    aux_chunks = 4 if args.aux_chunks is None else args.aux_chunks
+    # 1: 57.85-57.97 ms/step vs 58.03-58.14 for 0, 57.99-58.18 for 2, 58.18-58.32 for 3 and
+    # 58.34-58.43 for 4, three interleaved rounds on one box (profiles/r05/r05_c4_aux.log; round
+    # 4's library, whose factorisation hopped streams, preferred 4: r04j_c4aux.log)
+    aux_chunks = 1 if args.aux_chunks is None else args.aux_chunks
     fctx = kernels.FitPredictContext(dev, args.cross_start, args.aux_free_cus,
                                      aux_chunks) if args.c4_path == "fit_predict" else None
 
