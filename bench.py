@@ -266,13 +266,39 @@ def launch_ranks(args) -> int | None:
     N = 1) return None and run in-process."""
     if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
         return None
+    import signal
     import subprocess
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this host
+    # every rank's process group gives up on a missing peer well inside the wall limit
+    env.setdefault("GPFIT_PG_TIMEOUT_S", str(max(10, min(180, int(args.wall_limit * 0.6)))))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
            f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd, env=env)
+    # a fresh child in its own process group (no exec), so a hung rank can be ended with the
+    # whole group: a stalled collective leaves a JSON record and a non-zero code inside the
+    # driver's limit instead of running into it
+    t0 = time.perf_counter()
+    child = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return child.wait(timeout=args.wall_limit)
+    except subprocess.TimeoutExpired:
+        for sig, grace in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+            try:
+                os.killpg(child.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                child.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": args.gpus,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "error": f"ranks did not finish within --wall-limit "
+                                   f"{args.wall_limit:g} s; process group killed",
+                          "elapsed_s": round(time.perf_counter() - t0, 1)}), flush=True)
+        return 124
 
 
 def main_dry_run(args):
@@ -281,6 +307,8 @@ def main_dry_run(args):
     ctx = gdist.init_from_env("cpu", backend="gloo")
     if ctx.world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but {ctx.world} ranks joined")
+    if args.stall_rank == ctx.rank:       # testing only: a rank that never reaches the barrier
+        time.sleep(3600)
     gdist.barrier(ctx)
     t0 = time.perf_counter()
     gdist.barrier(ctx)
@@ -319,6 +347,12 @@ def main():
     ap.add_argument("--workload", choices=("c3", "c4", "fit", "latency"), default="c3")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rendezvous / JSON path only, no GPU work (gloo on the host)")
+    ap.add_argument("--wall-limit", type=float, default=540.0,
+                    help="--gpus N > 1 without a launcher: seconds before the ranks' process "
+                         "group is killed and a JSON error line printed (exit 124)")
+    ap.add_argument("--stall-rank", type=int, default=-1,
+                    help="testing only (--dry-run): this rank sleeps instead of joining the "
+                         "barrier")
     ap.add_argument("--latency-points", type=int, default=20,
                     help="latency: test points timed one at a time (time_predictions.py:68)")
     ap.add_argument("--ny", type=int, default=1347945, help="fit: field size per run")

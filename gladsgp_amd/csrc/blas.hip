@@ -418,8 +418,11 @@ __global__ __launch_bounds__(64 * kTskWaves, 8 / kTskWaves) void gemm_tsk_kernel
         }
       }
     };
+    // prologue: only groups inside the slice (FULL loads are unmasked: a group at or past ke
+    // would read up to 16 k past the slice, i.e. past X's last row and W's last k)
 #pragma unroll
-    for (int q = 0; q < R - 1; ++q) load(xr[q], bv[q], kb + G * q);
+    for (int q = 0; q < R - 1; ++q)
+      if (kb + G * q < ke) load(xr[q], bv[q], kb + G * q);
     for (int k0 = kb; k0 < ke; k0 += G * R) {
 #pragma unroll
       for (int q = 0; q < R; ++q) {
@@ -527,8 +530,11 @@ __global__ __launch_bounds__(256, TSM_OCC) void gemm_tsm_kernel(int M, int N, in
         }
       }
     };
+    // prologue: only groups < K (FULL loads are unmasked; K = 16 would otherwise read P's
+    // columns and Q's rows 16..31, past both operands)
 #pragma unroll
-    for (int q = 0; q < kTsRing - 1; ++q) load(a[q], bv[q], 16 * q);
+    for (int q = 0; q < kTsRing - 1; ++q)
+      if (16 * q < K) load(a[q], bv[q], 16 * q);
     for (int k0 = 0; k0 < K; k0 += 16 * kTsRing) {
 #pragma unroll
       for (int q = 0; q < kTsRing; ++q) {
@@ -652,7 +658,7 @@ __global__ __launch_bounds__(64 * kTskWaves, 8 / kTskWaves) void gemm_tsk16_kern
     };
     load_x(xr[0], kb);
     load_w(bv[0], kb);
-    load_x(xr[1], kb + G);
+    if (kb + G < ke) load_x(xr[1], kb + G);      // a 16-long slice has no second group
     for (int k0 = kb; k0 < ke; k0 += G * RX * RW) {
       static_for<0, RX * RW, 1>([&](auto Q) {
         constexpr int q = decltype(Q)::value;

@@ -16,6 +16,7 @@ sharding needs: one broadcast of the inputs and one gather of the outputs.
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 
@@ -37,7 +38,8 @@ class Context:
 
 
 def init_from_env(device_type: str | None = None, backend: str | None = None,
-                  device_index: int | None = None, force_group: bool = False) -> Context:
+                  device_index: int | None = None, force_group: bool = False,
+                  timeout_s: float | None = None) -> Context:
     """Join the process group described by RANK/WORLD_SIZE/MASTER_* (torchrun), if any.
 
     Defaults: one GPU per rank (cuda:LOCAL_RANK) over RCCL.  ``backend="gloo"`` with
@@ -45,7 +47,11 @@ def init_from_env(device_type: str | None = None, backend: str | None = None,
     collectives then stage through the host).  ``force_group``: join a process group even at
     world size 1 (RCCL accepts a one-rank communicator), so every collective branch of the
     sharded paths runs exactly as it does on N GPUs -- the one-GPU rehearsal of the RCCL code
-    path (``bench.py --force-nccl``, ``tests/test_gpu_rccl.py``)."""
+    path (``bench.py --force-nccl``, ``tests/test_gpu_rccl.py``).
+
+    ``timeout_s`` bounds the rendezvous and every collective of the group (default
+    ``GPFIT_PG_TIMEOUT_S`` or 180 s, well under a driver's 600 s bench limit): a rank that never
+    arrives makes the others raise instead of waiting out torch's default (10-30 min)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -72,7 +78,10 @@ def init_from_env(device_type: str | None = None, backend: str | None = None,
                 # the one-rank rehearsal (force_group): nobody else has to find this port
                 os.environ["MASTER_PORT"] = str(_free_port())
             kw = {"device_id": device} if backend == "nccl" else {}
-            dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+            if timeout_s is None:
+                timeout_s = float(os.environ.get("GPFIT_PG_TIMEOUT_S", "180"))
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
     else:
         backend = None
     return Context(rank, world, local_rank, device, backend)

@@ -19,6 +19,9 @@ Writes only data (.npz / .json / .csv) into tests/golden/:
   rank <= n - 1) float32 ensembles of n = 16, 20, 25 runs with ``init_model``'s
   ``r = min(25, n, ny)``, k = 0, q = 1 (``src/model.py:84``; ``test_install.sh`` uses
   ``--nsim 16``), seeded, with the Gaussian test matrices it drew.
+* ``svd_ref_pmax25.npz`` — the reference's ``randomized_svd`` called as ``init_model`` calls it
+  (``randomized_svd(y_std, 25, k=0, q=1)``, Omega (ny, 25)) on n = 16 and 20 runs, with the raw
+  ensemble, Omega and the global RNG's next value after the call.
 * ``c2_golden.npz`` — oracle GP outputs on the real 512x8 design (C2 recipe) at
   256 test points: Gram spot values, logdet, mean, var, nll.
 """
@@ -123,6 +126,43 @@ def svd_reference_deficient(ref: str) -> None:
     print("rank-deficient svd golden written")
 
 
+def svd_reference_model_call(ref: str) -> None:
+    """``svd_ref_pmax25.npz``: the reference's ``randomized_svd`` called exactly as
+    ``init_model`` calls it (``src/model.py:81-84``: ``pmax = 25``, ``randomized_svd(y_std, 25,
+    k=0, q=1)``) on column-centred float32 ensembles of n = 16 and 20 runs (fewer runs than
+    pmax: Omega is drawn (ny, 25), numpy's reduced QR keeps min(n, 25) = n columns, so U is
+    n x n, S n, Vh n x ny).  Stored: the raw float32 ensemble and design (so the build's own
+    ``init_model`` runs on it), the float32 y_std the reference standardised (src/model.py:60-72),
+    the drawn Omega, the reference's U / S / Vh, and the first ``np.random.random()`` after the
+    call (the global RNG's advance)."""
+    spec = importlib.util.spec_from_file_location("ref_svd", os.path.join(ref, "src", "svd.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = {}
+    ny = 400
+    for n in (16, 20):
+        rng = np.random.default_rng(200 + n)
+        t = rng.random((n, 8)).astype(np.float32)
+        modes = rng.standard_normal((8, ny)) * (0.7 ** np.arange(8))[:, None]
+        coef = np.stack([np.sin(2 * np.pi * t @ rng.uniform(0, 1, 8) + k) for k in range(8)], 1)
+        y = (3.0 + coef @ modes + 1e-2 * rng.standard_normal((n, ny))).astype(np.float32)
+        mu = np.mean(y, axis=0)                      # src/model.py:60-72, in y's dtype
+        sd = np.std(y, ddof=1, axis=0)
+        sd[sd < 1e-6] = 1e-6
+        y_std = (y - mu) / sd
+        np.random.seed(2000 + n)
+        U, S, Vh = mod.randomized_svd(y_std, 25, k=0, q=1)
+        after = np.random.random()
+        np.random.seed(2000 + n)
+        omega = np.random.normal(size=(ny, 25)).astype(np.float32)
+        assert U.shape == (n, n) and S.shape == (n,) and Vh.shape == (n, ny)
+        out.update({f"n{n}_t": t, f"n{n}_y": y, f"n{n}_y_std": y_std, f"n{n}_omega": omega,
+                    f"n{n}_U": U, f"n{n}_S": S, f"n{n}_Vh": Vh,
+                    f"n{n}_next_random": np.float64(after), f"n{n}_seed": np.int64(2000 + n)})
+    np.savez_compressed(os.path.join(HERE, "svd_ref_pmax25.npz"), **out)
+    print("pmax=25 model-call svd golden written")
+
+
 def c2_golden() -> None:
     X = np.loadtxt(os.path.join(HERE, "synthetic_train_standard.csv"), delimiter=",",
                    skiprows=1, comments=None)
@@ -153,6 +193,7 @@ def main() -> None:
     notebook_known_answer(args.reference)
     svd_reference(args.reference)
     svd_reference_deficient(args.reference)
+    svd_reference_model_call(args.reference)
     c2_golden()
 
 

@@ -200,6 +200,43 @@ def test_bench_gpus_flag_launches_ranks():
     assert r.returncode != 0 and "2 but 1 ranks" in r.stderr
 
 
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("mode", ["wall_limit", "pg_timeout"])
+def test_bench_stalled_rank_fails_loudly(mode):
+    """A rank that never reaches a collective must not hang ``bench.py --gpus 2``: either the
+    process group's timeout (dist.init_from_env, ~0.6 x --wall-limit under the launcher) makes
+    the waiting rank raise, or the launcher's wall limit kills the ranks' process group and
+    prints a JSON error line; both exit non-zero well inside the limit."""
+    import json
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+                        "GPFIT_PG_TIMEOUT_S")}
+    if mode == "wall_limit":
+        env["GPFIT_PG_TIMEOUT_S"] = "900"          # only the wall limit can end it
+        limit = 20
+    else:
+        limit = 30                                  # process-group timeout 18 s
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--dry-run", "--stall-rank", "1", "--wall-limit", str(limit)],
+                       capture_output=True, text=True, env=env, timeout=200)
+    elapsed = time.perf_counter() - t0
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert elapsed < limit + 40, elapsed
+    if mode == "wall_limit":
+        assert r.returncode == 124
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        rec = json.loads(lines[0])
+        assert rec["value"] is None and "wall-limit" in rec["error"] and rec["n_gpus"] == 2
+    else:
+        assert elapsed < limit, elapsed
+
+
 def test_balanced_split_minimises_the_slowest_rank():
     """sharded.balanced_split against brute force on a staircase prediction time (the TRMM's
     residency rounds: 4096 points per round, a partial round at 0.65 of a full one)."""

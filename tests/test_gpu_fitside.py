@@ -24,7 +24,16 @@ def _t(a, dev):
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (70, 33, 129), (128, 64, 64), (17, 5, 60000),
-                                   (512, 25, 70001), (20001, 25, 300), (25, 20001, 300)])
+                                   (512, 25, 70001), (20001, 25, 300), (25, 20001, 300),
+                                   # tsm / tsm_t with the narrow side below one 16-wide MFMA
+                                   # column tile (blas.hip's clamped column indices)
+                                   (20001, 7, 300), (7, 20001, 300), (20001, 1, 300),
+                                   (15, 20001, 300),
+                                   # K = 16: one K-group, the prologue must not prefetch a second
+                                   (16, 20001, 16), (20001, 16, 16),
+                                   # tsk with a last K-slice of 8 (tsk_shape at m = 512: 288-long
+                                   # slices, 69992 = 243 * 288 + 8)
+                                   (512, 7, 69992)])
 def test_gemm(dev, ta, tb, m, n, k):
     from gladsgp_amd.blas import CM, gemm
     rng = np.random.default_rng(m + n + k + ta * 2 + tb)
@@ -49,7 +58,12 @@ def test_gemm(dev, ta, tb, m, n, k):
                                    (25, 20001, 300), (32, 9000, 512),
                                    # even leading dimensions: the fp64 tsk runs take the
                                    # 16-B tsk16 form, the float32 runs the 8-B one
-                                   (512, 25, 70000), (20000, 25, 300)])
+                                   (512, 25, 70000), (20000, 25, 300),
+                                   # narrow side < 16 (tsm, tsm_t), K = 16, a last tsk slice of
+                                   # 8 (69992) or 16 (70000 above) k
+                                   (20001, 7, 300), (7, 20001, 300), (20001, 15, 300),
+                                   (1, 20001, 300), (16, 20001, 16), (20001, 16, 16),
+                                   (512, 25, 69992), (512, 7, 70000)])
 def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
     """gp_gemm_ex with a float32 A and/or B (widened on load) equals gp_gemm_ex / gp_dgemm on
     fp64 copies of the same values bit for bit, split-K shapes included (512 x 25 x 40000 is
@@ -78,8 +92,8 @@ def test_gemm_float32_operands_bit_identical(dev, ta, tb, m, n, k):
 
 
 @pytest.mark.parametrize("kind", ["tsk", "tsm", "tsm_t"])
-@pytest.mark.parametrize("big", [70001, 20001])
-def test_tall_skinny_padded_ld_matches_unpadded(dev, kind, big):
+@pytest.mark.parametrize("big,runs", [(70001, None), (20001, None), (20001, 16), (70000, 16)])
+def test_tall_skinny_padded_ld_matches_unpadded(dev, kind, big, runs):
     """The ensemble's padded row stride (emulator.standardize_y) selects the 16-B tsk form
     (blas.hip tsk16); every tall-skinny product on the padded ensemble equals the one on an
     unpadded copy bit for bit, odd lengths (a 16-B pair straddling the row end, zeroed)
@@ -87,8 +101,11 @@ def test_tall_skinny_padded_ld_matches_unpadded(dev, kind, big):
     from gladsgp_amd.blas import CM, gemm
     if kind == "tsk" and big < 65536:
         pytest.skip("tsk needs K >= 65536")
-    rng = np.random.default_rng(big + len(kind))
-    runs, r = 300 if kind != "tsk" else 512, 25
+    rng = np.random.default_rng(big + len(kind) + (runs or 0))
+    # runs = 16: the reference's test_install.sh ensemble (--nsim 16), K = 16 for tsm / tsm_t
+    r = 25
+    if runs is None:
+        runs = 300 if kind != "tsk" else 512
     X = rng.standard_normal((runs, big))                 # C-order ensemble: runs x locations
     ld = (big + 15) // 16 * 16
     pad = torch.full((runs, ld), float("nan"), dtype=torch.float64, device=dev)
@@ -303,3 +320,36 @@ def test_init_model_caches_reference_dtype(dev, tmp_path):
                       verbose=False)
         for a in ("U", "S", "Vh"):
             assert np.load(d / f"pca_dt_{a}.npy").dtype == dt
+
+
+@pytest.mark.parametrize("n", [16, 20])
+def test_init_model_matches_reference_pmax25_call(dev, golden_dir, tmp_path, n):
+    """The build's init_model (n < 25 runs: Omega's first n columns, gladsgp_amd/model.py)
+    against the reference's randomized_svd called as src/model.py:81-84 calls it
+    (tests/golden/svd_ref_pmax25.npz: pmax = 25, Omega (ny, 25)): cached S to rtol on the n - 1
+    nonzero values, U / Vh up to sign on the leading well-separated vectors, the same cached
+    shapes and dtypes, and the same advance of numpy's global RNG."""
+    from gladsgp_amd import model as gm
+    g = np.load(os.path.join(golden_dir, "svd_ref_pmax25.npz"))
+    t, y = g[f"n{n}_t"], g[f"n{n}_y"]
+    ny = y.shape[1]
+    np.random.seed(int(g[f"n{n}_seed"]))
+    gm.init_model(t, y, "pm", 5, data_dir=str(tmp_path), device=dev, verbose=False)
+    assert np.random.random() == float(g[f"n{n}_next_random"])
+    U = np.load(tmp_path / "pca_pm_U.npy")
+    S = np.load(tmp_path / "pca_pm_S.npy")
+    Vh = np.load(tmp_path / "pca_pm_Vh.npy")
+    S_ref, U_ref, Vh_ref = g[f"n{n}_S"], g[f"n{n}_U"], g[f"n{n}_Vh"]
+    assert U.shape == U_ref.shape == (n, n) and S.shape == S_ref.shape == (n,)
+    assert Vh.shape == Vh_ref.shape == (n, ny)
+    assert U.dtype == S.dtype == Vh.dtype == np.float32
+    np.testing.assert_allclose(S[: n - 1], S_ref[: n - 1], rtol=2e-4, atol=1e-4 * S_ref[0])
+    assert S[-1] <= 1e-4 * S[0]
+    checked = 0
+    for i in range(4):
+        if S_ref[i] - S_ref[i + 1] > 1e-2 * S_ref[0]:
+            sg = np.sign(U[:, i] @ U_ref[:, i])
+            np.testing.assert_allclose(sg * U[:, i], U_ref[:, i], atol=1e-3)
+            np.testing.assert_allclose(sg * Vh[i], Vh_ref[i], atol=1e-3)
+            checked += 1
+    assert checked >= 2
