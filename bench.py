@@ -344,7 +344,11 @@ def main():
     ap.add_argument("--cpu-faithful-batches", type=int, default=10,
                     help="reference-faithful CPU leg: batches of 4 test points timed "
                          "(assess_all_models.py:481-489 re-factorises per batch)")
-    ap.add_argument("--workload", choices=("c3", "c4", "fit", "latency"), default="c3")
+    ap.add_argument("--workload", choices=("c3", "c4", "c5", "fit", "latency"), default="c3")
+    ap.add_argument("--c5-ny", type=int, default=10000, help="c5: field nodes")
+    ap.add_argument("--c5-pcs", type=int, default=64, help="c5: principal components")
+    ap.add_argument("--c5-cpu-sample", type=int, default=3000,
+                    help="c5: test points the CPU oracle predicts (all PCs) and reconstructs")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rendezvous / JSON path only, no GPU work (gloo on the host)")
     ap.add_argument("--wall-limit", type=float, default=540.0,
@@ -381,6 +385,8 @@ def main():
         return main_dry_run(args)
     if args.workload == "c4":
         return main_c4(args)
+    if args.workload == "c5":
+        return main_c5(args)
     if args.workload == "fit":
         return main_fit(args)
     if args.workload == "latency":
@@ -877,6 +883,209 @@ def cpu_latency_baseline(data, model, samples, xi, sd_y, reps: int = 3):
                        f"{_CPU_THREADS} threads on {cpu_model()}: one time_predictions.py "
                        f"iteration (S x P = {w_hat.shape[1] * len(samples['lamUz'])} GPs at "
                        f"n = {t.shape[0]}, field of {K.shape[1]} nodes), median of {reps}")}
+
+
+def main_c5(args):
+    """BASELINE config 5: the synthetic GlaDS ensemble through the whole chained
+    surface, one step = gladsgp_amd.pipeline.FieldPipeline.run():
+      standardise the 512 x 10k float32 field (src/model.py:60-72) -> randomized_svd(Y_std, 64,
+      k=0, q=1) (plot_PC_RMSE.py:90-91) -> K = diag(S) Vh / sqrt(n), w_hat, LamSim
+      (src/model.py:101, 219) -> the 64 PC GPs at m = 100k test points, mean + variance
+      (SepiaEmulatorPrediction, assess_all_models.py:487-489) -> preds.w float32,
+      get_y() = the 100k x 10k field on the device (assess_all_models.py:490-492).
+    value = S x P x m posterior predictions per step / step time (every step redoes every
+    phase from the raw field).  N > 1: inputs broadcast once at setup, every rank runs the
+    cheap SVD / basis redundantly, the PC GPs are dealt round-robin with one gather of (mean,
+    var) to rank 0, and the field is reconstructed in ny-column blocks after one broadcast of w
+    (each rank keeps its block)."""
+    from gladsgp_amd.pipeline import FieldPipeline, synthetic_c5
+    ctx = gdist.init_from_env("cuda", force_group=args.force_nccl)
+    if ctx.world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but {ctx.world} ranks joined")
+    dev = ctx.device
+    n, d, ny, m, P = 512, args.d, args.c5_ny, args.m, args.c5_pcs
+    if ctx.rank == 0:
+        t, Y, omega, smp, t_pred = synthetic_c5(n, d, ny, m, P)
+        host = [t, Y, omega, t_pred] + [smp[k] for k in ("betaU", "lamUz", "lamWs", "lamWOs")]
+        bufs = [torch.as_tensor(np.ascontiguousarray(a), device=dev) for a in host]
+    else:
+        shapes = [((n, d), torch.float64), ((n, ny), torch.float32), ((ny, P), torch.float32),
+                  ((m, d), torch.float64), ((1, (d + 1) * P), torch.float64),
+                  ((1, P), torch.float64), ((1, P), torch.float64), ((1, 1), torch.float64)]
+        bufs = [torch.empty(sh, dtype=dt, device=dev) for sh, dt in shapes]
+    for b in bufs:                                   # one broadcast per input, at setup
+        gdist.broadcast_(ctx, b)
+    t_d, Y_d, om_d, tp_d = bufs[:4]
+    smp = {k: v.cpu().numpy() for k, v in zip(("betaU", "lamUz", "lamWs", "lamWOs"), bufs[4:])}
+    S = smp["lamUz"].shape[0]
+    pipe = FieldPipeline(t_d, Y_d, om_d, smp, tp_d, P, device=dev,
+                         ctx=ctx if ctx.distributed else None, m_chunk=args.m_chunk,
+                         aux_chunks=1 if args.aux_chunks is None else args.aux_chunks)
+    res = None
+    for _ in range(args.warmup):
+        res = pipe.run()
+    torch.cuda.synchronize()
+    _capi.call("gp_profile_enable", 64 * (args.steps + 1) * P)
+    select = getattr(_capi.lib(), "gp_profile_select", lambda mask: 0)
+    select(1 << _capi.PROF_TRMM)
+    _capi.call("gp_profile_reset")
+    gdist.barrier(ctx)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = pipe.run()
+    torch.cuda.synchronize()
+    gdist.barrier(ctx)
+    elapsed = gdist.max_over_ranks(ctx, time.perf_counter() - t0)
+    tr_cnt, tr_ms = read_prof(_capi.PROF_TRMM)
+    select(0xFFFFFFFF)
+    _capi.call("gp_profile_enable", 0)
+    # per-phase device times: events on the pipeline's stream over two untimed steps after the
+    # timed region (event pairs inside it would add their own waits)
+    phase_steps = 2
+    ph = {}
+    for _ in range(phase_steps):
+        pipe.events = []
+        res = pipe.run()
+        torch.cuda.synchronize()
+        evs = pipe.events
+        for (a, ea), (b, eb) in zip(evs[:-1], evs[1:]):
+            ph[b] = ph.get(b, 0.0) + ea.elapsed_time(eb) / phase_steps
+    pipe.events = None
+    if ctx.rank != 0:
+        pipe.close()
+        return
+    K = args.steps
+    preds = S * P * m
+    value = preds * K / elapsed
+    bl = len(gdist.shard_units(S * P, 0, ctx.world))
+    tr_flops = float(bl) * m * K * (n * n + 4 * n)
+    tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12 if tr_ms > 0 else 0.0
+    y = res["y"]
+    ny_r = y.shape[-1]
+    svd_bytes = 4.0 * n * ny * 8 + ny * P * 4          # y_std read by the 4 ensemble products
+    svd_s = ph["svd"] * 1e-3
+    fy_s = ph["get_y"] * 1e-3
+    fy_flop = 2.0 * S * m * ny_r * P
+    fy_bytes = S * m * ny_r * y.element_size() + S * m * P * 8 + P * ny_r * 8
+    pr_s = ph["predict"] * 1e-3
+    line = {
+        "metric": "GP posterior predictions/sec fp64, C5 synthetic GlaDS ensemble (n=512 d=8, "
+                  f"{ny}-node field, {P} PCs via randomized_svd, m={m}, field reconstructed)",
+        "value": value, "unit": "predictions/s", "n_gpus": ctx.world, "steps": K,
+        "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64 (SVD, GP); field stored f32 after the reference's .w.astype(float32)",
+        "data": "synthetic (SURVEY §8d C5: the reference's Sobol 512x8 design, seeded smooth "
+                "96-mode float32 field + 1e-3 noise, Omega drawn as src/svd.py:51 after "
+                "np.random.seed(0), GPMSA-typical hyperparameters, X* = rng(2))",
+        "config": {"workload": "C5: standardise -> randomized_svd(Y_std, 64, k=0, q=1) -> K, "
+                               "w_hat -> 64 PC GPs at m test points (mean + var) -> preds.w "
+                               "float32 -> get_y() field on the device",
+                   "n_train": n, "d": d, "ny": ny, "pcs": P, "samples": S, "m_test": m,
+                   "field_shape": [S, m, ny],
+                   "parallelism": (f"PC shards x{ctx.world} (units round-robin, gather of "
+                                   "(mean, var) to rank 0) + ny-column field blocks after a "
+                                   "broadcast of w; SVD / basis redundant per rank"
+                                   if ctx.distributed else "1 GPU"),
+                   "collectives": (f"{ctx.backend} process group of {ctx.world}"
+                                   if ctx.distributed else "none (single process)")},
+        "phases_ms": {k: round(v, 4) for k, v in ph.items()},
+        "roofline": {"kernel": "trmm_pair_kernel (the PC GPs' TRMM)", "bound": "mfma",
+                     "achieved": round(tr_tfs, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": None, "launches": tr_cnt,
+                     "avg_launch_ms": round(tr_ms / max(tr_cnt, 1), 4),
+                     "flop_per_launch": tr_flops / max(tr_cnt, 1),
+                     "work_note": "n^2 + 4n flop per prediction"},
+        "roofline_phases": {
+            "svd": {"bound": "hbm", "achieved": round(svd_bytes / svd_s / 1e9, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(svd_bytes / svd_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "ms": round(ph["svd"], 4),
+                    "work_note": "4 reads of the fp64 y_std (X Omega, Y^T X, X Z, Q^T X) + "
+                                 "Omega; the phase also holds CholeskyQR3, the Jacobi "
+                                 "eigensolver and their host checks (latency at this size)"},
+            "predict": {"bound": "mfma",
+                        "achieved": round(float(bl) * m * (n * n + 4 * n) / pr_s / 1e12, 3),
+                        "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(float(bl) * m * (n * n + 4 * n) / pr_s / 1e12
+                                      / FP64_MFMA_PEAK_TFLOPS, 4),
+                        "ms": round(ph["predict"], 4),
+                        "work_note": "whole EmulatorPrediction phase (Gram, factorisation, "
+                                     "cross-covariance, TRMM, finalize, gather) at the TRMM's "
+                                     "n^2 + 4n flop per prediction"},
+            "get_y": {"bound": "mfma", "achieved": round(fy_flop / fy_s / 1e12, 3),
+                      "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": round(fy_flop / fy_s / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                      "hbm_achieved_gbs": round(fy_bytes / fy_s / 1e9, 1),
+                      "hbm_frac": round(fy_bytes / fy_s / 1e9 / HBM_PEAK_GBS, 4),
+                      "ms": round(ph["get_y"], 4),
+                      "work_note": f"2P = {2 * P} fp64 MFMA flop and {y.element_size()} B "
+                                   "written per field element (+ w and K read): the fp64 "
+                                   "product bounds it (1.63 ms at peak vs 0.5 ms of writes at "
+                                   "C5); gp_field"},
+        },
+        "cpu_baseline": None,
+    }
+    if ctx.world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_c5(pipe, res, args.c5_cpu_sample)
+    pipe.close()
+    print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_c5(pipe, res, sample: int):
+    """The oracle on the host for C5: standardise + randomized_svd (same Omega) + basis + PC
+    weights in full, then all P PC GPs (gp_ref.sepia_predict_w) and the field y = (w K) sd + mu
+    for the first ``sample`` test points, extrapolated linearly in the points to m.  Parity:
+    the oracle's singular values against the GPU's; the GPs and the field on the GPU's own basis
+    K (singular vectors are unique up to sign: the GP means follow K's signs) against the GPU's
+    mean / var / field rows."""
+    from oracle import gp_ref
+    t = pipe.t.cpu().numpy()
+    Y = pipe.y.cpu().numpy()
+    om = pipe.omega.cpu().numpy()
+    tp = pipe.t_pred[:sample].cpu().numpy()
+    n, P, m = t.shape[0], pipe.p, pipe.t_pred.shape[0]
+    K_gpu = res["K"].cpu().numpy()
+    t0 = time.perf_counter()
+    mu, sd, ys = gp_ref.standardize(Y)
+    _, S_o, Vh_o = gp_ref.randomized_svd(ys, P, k=0, q=1, omega=om)
+    K_o = (gp_ref.pca_basis(S_o, Vh_o, P, n)).astype(np.float32).astype(np.float64)
+    w_o = gp_ref.pc_weights(ys, K_o)
+    t_basis = time.perf_counter() - t0
+    w_hat = gp_ref.pc_weights(ys, K_gpu)                  # the GP inputs on the GPU's basis
+    lam = np.sum(K_gpu * K_gpu, axis=1)
+    t1 = time.perf_counter()
+    mean, var = gp_ref.sepia_predict_w(t, tp, w_hat, pipe.samples, lam)
+    y_o = (np.einsum("smp,py->smy", mean.astype(np.float32).astype(np.float64), K_gpu)
+           * sd + mu).astype(np.float32)
+    t_pts = time.perf_counter() - t1
+    del w_o
+    t_full = t_basis + t_pts / sample * m
+    S = mean.shape[0]
+    g_mean = res["mean"][:, :sample].cpu().numpy()
+    g_var = res["var"][:, :sample].cpu().numpy()
+    g_y = res["y"][:, :sample].cpu().numpy()
+    S_g = res["S"].cpu().numpy()
+    sgn = np.sign(np.sum(K_gpu * K_o, axis=1))
+    return {"value": S * P * m / t_full, "unit": "predictions/s", "cores": _CPU_THREADS,
+            "kind": "port",
+            "sample": (f"oracle/gp_ref numpy fp64, OpenBLAS {_CPU_THREADS} threads on "
+                       f"{cpu_model()}: standardise + randomized_svd + basis + PC weights in "
+                       f"full ({t_basis:.2f} s), then all {P} PC GPs and the field for the first "
+                       f"{sample} of {m} test points ({t_pts:.2f} s), extrapolated linearly in "
+                       f"the points to m"),
+            "parity_vs_gpu": {
+                "points": sample,
+                "max_rel_dS": float(np.max(np.abs(S_g - S_o) / S_o)),
+                "max_abs_dK_signed": float(np.max(np.abs(K_gpu * sgn[:, None] - K_o))),
+                "max_abs_dmean": float(np.max(np.abs(g_mean - mean))),
+                "max_abs_dvar": float(np.max(np.abs(g_var - var))),
+                "max_abs_dfield": float(np.max(np.abs(g_y.astype(np.float64) - y_o))),
+                "max_abs_field": float(np.max(np.abs(y_o))),
+                "note": "mean / var / field on the GPU's basis K; S and K against the oracle's "
+                        "own SVD (K up to each PC's sign)"}}
 
 
 # reference fit timings (BASELINE.md; timing.csv:9, n=512 P=8: PCA incl. load/standardise,

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libgpfit.so")
 # the persistent factorisation's timestamp trace compiled in (-DGPFIT_PP_TRACE).
 TRACE_LIB_PATH = os.path.join(PKG_DIR, "libgpfit_trace.so")
 SOURCES = ["gram.hip", "chol.hip", "predict.hip", "linalg.hip", "profile.hip", "blas.hip",
-           "eig.hip", "comm.hip", "rng.hip", "mcmc.hip", "host_rng.hip"]
+           "eig.hip", "comm.hip", "rng.hip", "mcmc.hip", "host_rng.hip", "field.hip"]
 # Per-file extra flags.  chol.hip: MFMA accumulators in VGPRs (not AGPRs) so the update
 # kernel, whose lookahead block calls the ~250-VGPR diagonal factor, keeps 2 waves/SIMD; and
 # 16-byte LDS reads (ds_read_b128) for the factor's broadcast rows.

@@ -108,6 +108,9 @@ SIGNATURES = {
     "gp_standardize": (c_int, [c_void_p, c_int, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_ll,
                                c_int, c_void_p]),
     "gp_mean_var": (c_int, [c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p]),
+    "gp_field_max_pcs": (c_int, []),
+    "gp_field": (c_int, [c_void_p, c_ll, c_int, c_int, c_void_p, c_ll, c_int, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
     "gp_shift_diag": (c_int, [c_void_p, c_int, c_int, ctypes.c_double, c_void_p]),
     "gp_rowscale": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "gp_syevj": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int,

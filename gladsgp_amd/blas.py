@@ -122,6 +122,38 @@ def standardize(Y: torch.Tensor, mu: torch.Tensor, sd: torch.Tensor, inverse: bo
     return out
 
 
+def field_max_pcs() -> int:
+    return int(_capi.lib().gp_field_max_pcs())
+
+
+def field(W: torch.Tensor, K: torch.Tensor, sd: torch.Tensor | None = None,
+          mu: torch.Tensor | None = None, err: torch.Tensor | None = None, f32: bool = False,
+          out: torch.Tensor | None = None) -> torch.Tensor:
+    """Y = (W K + err) sd + mu in one pass (gp_field; SepiaEmulatorPrediction.get_y):
+    W (rows x P) and K (P x ncols, row stride free) row-major fp64 on the device, sd / mu
+    (ncols) or both None (standardised field), err (rows) or None; Y (rows x ncols) float32 when
+    ``f32`` else float64."""
+    rows, P = W.shape
+    if K.shape[0] != P or K.stride(1) != 1 or W.stride(1) != 1:
+        raise ValueError("field: W (rows x P) and K (P x ncols) must be row-major, K.shape[0] = P")
+    ncols = K.shape[1]
+    if out is None:
+        out = torch.empty((rows, ncols), dtype=torch.float32 if f32 else F64, device=W.device)
+    if (sd is None) != (mu is None):
+        raise ValueError("field: sd and mu go together")
+    for t in (sd, mu, err):
+        if t is not None and (t.dtype != F64 or not t.is_contiguous()):
+            raise ValueError("field: sd / mu / err must be contiguous float64")
+    if err is not None and err.numel() != rows:
+        raise ValueError(f"field: err has {err.numel()} values for {rows} rows")
+    _capi.call("gp_field", W.data_ptr(), W.stride(0), rows, P, K.data_ptr(), K.stride(0), ncols,
+               sd.data_ptr() if sd is not None else None,
+               mu.data_ptr() if mu is not None else None,
+               err.data_ptr() if err is not None else None, out.data_ptr(), out.stride(0),
+               int(f32), _stream(W.device))
+    return out
+
+
 def mean_var(x: torch.Tensor, ddof: int = 0):
     """(mean, var) of all elements of ``x`` (device scalars tensor of 2)."""
     x = x.contiguous()

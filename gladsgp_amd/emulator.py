@@ -147,7 +147,9 @@ class EmulatorData:
 
     def create_K_basis(self, K):
         """Set the PCA basis K (P x ny) — SEPIA create_K_basis (model.py:102)."""
-        self.sim_data.K = torch.as_tensor(_np(K), dtype=F64, device=self.device).contiguous()
+        self.sim_data.K = (K.to(device=self.device, dtype=F64).contiguous() if torch.is_tensor(K)
+                           else torch.as_tensor(np.asarray(K), dtype=F64,
+                                                device=self.device).contiguous())
 
 
 def pc_weights(data: EmulatorData):
@@ -299,12 +301,15 @@ def gp_params(samples, LamSim, d, P, pred_nugget=True):
 
 
 def predict_units(X, Xs, w_units, beta_u, s_u, delta_u, sp_u, budget_bytes=2 << 30,
-                  m_chunk=0, group=None):
+                  m_chunk=0, group=None, fctx: kernels.FitPredictContext | None = None,
+                  workspace: kernels.PredictWorkspace | None = None):
     """Posterior mean / variance of a list of GPs sharing X and Xs: returns (U, m) x 2.
 
     Units are processed in groups bounded by ``budget_bytes`` of Gram + L^-1 storage, and by
-    ``group`` GPs per group when given (each group is one batched Gram -> factorisation ->
-    prediction).
+    ``group`` GPs per group when given; each group is one gp_fit_predict (batched Gram ->
+    factorisation -> cross-covariance / TRMM / mean + variance), whose cross-covariance runs on
+    ``fctx``'s own stream beside the factorisation when a context is given (bit-identical to
+    gram -> potrf -> predict on one stream: tests/test_gpu_c4.py).
     """
     dev = X.device
     U = beta_u.shape[0]
@@ -317,15 +322,12 @@ def predict_units(X, Xs, w_units, beta_u, s_u, delta_u, sp_u, budget_bytes=2 << 
         g = max(1, min(g, int(group)))
     mean = torch.empty((U, m), dtype=F64, device=dev)
     var = torch.empty((U, m), dtype=F64, device=dev)
-    ws = kernels.PredictWorkspace()
+    ws = workspace if workspace is not None else kernels.PredictWorkspace()
     for a in range(0, U, g):
         b = min(U, a + g)
-        G = kernels.gram(X, beta_u[a:b], s_u[a:b], delta_u[a:b], batch=b - a)
-        ch = kernels.cholesky_inverse(G)
-        ch.check()
-        kernels.predict(ch, X, Xs, beta_u[a:b], s_u[a:b], sp_u[a:b], w_units[a:b],
-                        m_chunk=m_chunk, workspace=ws, out=(mean[a:b], var[a:b]))
-        del G, ch
+        kernels.fit_predict(X, Xs, beta_u[a:b], s_u[a:b], delta_u[a:b], sp_u[a:b],
+                            w_units[a:b], m_chunk=m_chunk, workspace=ws,
+                            out=(mean[a:b], var[a:b]), ctx=fctx, check=True)
     return mean, var
 
 
@@ -341,19 +343,24 @@ class EmulatorPrediction:
         are split instead, every rank predicting every unit on its contiguous block
         (``shard="points"``, SURVEY §8e single-output GP; see gladsgp_amd.sharded).
     ``shard`` forces "units" or "points".  ``group`` caps the GPs per batched factorisation.
+    ``fctx`` / ``workspace``: a caller-owned gp_fit_predict context (cross-covariance beside the
+    factorisation) and prediction workspace, reused across calls.
     """
 
     def __init__(self, model: EmulatorModel = None, samples: dict = None, t_pred=None,
                  pred_nugget: bool = True, ctx: gdist.Context | None = None,
                  budget_bytes: int = 2 << 30, m_chunk: int = 0, realize: bool = False,
-                 seed: int | None = None, group: int | None = None, shard: str | None = None):
+                 seed: int | None = None, group: int | None = None, shard: str | None = None,
+                 fctx: kernels.FitPredictContext | None = None,
+                 workspace: kernels.PredictWorkspace | None = None):
         if model is None or samples is None or t_pred is None:
             raise ValueError("EmulatorPrediction needs model, samples and t_pred")
         self.model = model
         dev = model.device
         X = model.data.sim_data.t_dev
-        Xs = torch.as_tensor(_np(t_pred), dtype=F64, device=dev).reshape(-1, model.d)
-        Xs = Xs.contiguous()
+        Xs = (t_pred.to(device=dev, dtype=F64) if torch.is_tensor(t_pred) else
+              torch.as_tensor(np.asarray(t_pred), dtype=F64, device=dev))
+        Xs = Xs.reshape(-1, model.d).contiguous()
         beta, s, delta, sp = gp_params(samples, _np(model.LamSim), model.d, model.P,
                                        pred_nugget)
         S, P = s.shape
@@ -378,7 +385,7 @@ class EmulatorPrediction:
             mean_l, var_l = predict_units(X, Xs[lo:hi].contiguous(), w_hat[jj].contiguous(),
                                           t(beta[sel_s, sel_j]), t(s[sel_s, sel_j]),
                                           t(delta[sel_s, sel_j]), t(sp[sel_s, sel_j]),
-                                          budget_bytes, m_chunk, group)
+                                          budget_bytes, m_chunk, group, fctx, workspace)
         else:
             mine = gdist.shard_units(len(units), rank, world)
             if mine:
@@ -388,7 +395,7 @@ class EmulatorPrediction:
                 mean_l, var_l = predict_units(X, Xs, w_hat[jj].contiguous(),
                                               t(beta[sel_s, sel_j]), t(s[sel_s, sel_j]),
                                               t(delta[sel_s, sel_j]), t(sp[sel_s, sel_j]),
-                                              budget_bytes, m_chunk, group)
+                                              budget_bytes, m_chunk, group, fctx, workspace)
             else:
                 mean_l = torch.empty((0, self.m), dtype=F64, device=dev)
                 var_l = torch.empty((0, self.m), dtype=F64, device=dev)
@@ -458,7 +465,8 @@ class EmulatorPrediction:
         return rng.standard_normal((self.S, cols)) / np.sqrt(self.lamWOs)[:, None]
 
     def get_y(self, std: bool = False, w=None, add_error: bool = False, rng=None,
-              per_point: bool = True, ctx="inherit", gather: bool = True):
+              per_point: bool = True, ctx="inherit", gather: bool = True,
+              to_host: bool = True):
         """Field reconstruction y = (w K) sd + mu, shape (S, m, ny) — SEPIA get_y().
 
         ``add_error`` adds the reference's PC-truncation error term (error_draws, times sd_y
@@ -469,6 +477,10 @@ class EmulatorPrediction:
         ``shard_range(ny, r, N)`` with its slice of K, and with ``gather`` rank 0 receives the
         whole (S, m, ny) field (other ranks None); ``gather=False`` returns every rank's own
         (S, m, ny_r) column block (``self.y_cols`` holds its range).
+
+        ``to_host=False`` returns the device tensor instead of numpy (no PCIe copy).  With at
+        most gp_field_max_pcs() PCs the product, error term, back-transform and narrowing are
+        one kernel (gp_field: every output element written once, in its final dtype).
         """
         sd_ = self.model.data.sim_data
         dev = self.model.device
@@ -492,11 +504,7 @@ class EmulatorPrediction:
             c0, c1 = 0, sd_.K.shape[1]
         out_dtype = np.float32 if f32 else np.float64
         self.y_cols = (c0, c1)
-        K = sd_.K if (c0, c1) == (0, sd_.K.shape[1]) else sd_.K[:, c0:c1].contiguous()
-        Wc = CM.of_rowmajor(wd.reshape(S * m, P).contiguous())   # (P x S m)
-        Kc = CM.of_rowmajor(K)                                   # (ny_r x P)
-        Yc = gemm(False, False, Kc, Wc)                          # (ny_r x S m) = (w K)^T
-        y = Yc.t[: S * m, : c1 - c0]                             # (S m, ny_r) row-major
+        e = None
         if add_error:
             cols = m if per_point else 1
             if not dist_on or ctx.rank == 0:
@@ -505,16 +513,32 @@ class EmulatorPrediction:
                 e = torch.empty((S, cols), dtype=F64, device=dev)
             if dist_on:
                 gdist.broadcast_(ctx, e)
-            e = e.expand(S, m) if e.shape[1] == 1 else e
-            y = y + e.reshape(S * m, 1)                          # one scalar per row
+            e = (e.expand(S, m) if e.shape[1] == 1 else e).reshape(S * m).contiguous()
+        mu = sd = None
         if not std:
             mu, sd = sd_.y_mean[c0:c1].contiguous(), sd_.y_sd[c0:c1].contiguous()
-            y = blas.standardize(y.contiguous(), mu, sd, inverse=True)
+        w2 = wd.reshape(S * m, P).contiguous()
+        if P <= blas.field_max_pcs():
+            # one pass: y = (w K + e) sd + mu, written once in the output dtype (K's column
+            # block read in place through its row stride)
+            y = blas.field(w2, sd_.K[:, c0:c1], sd, mu, e, f32=f32)
+        else:
+            K = sd_.K if (c0, c1) == (0, sd_.K.shape[1]) else sd_.K[:, c0:c1].contiguous()
+            Wc = CM.of_rowmajor(w2)                              # (P x S m)
+            Kc = CM.of_rowmajor(K)                               # (ny_r x P)
+            Yc = gemm(False, False, Kc, Wc)                      # (ny_r x S m) = (w K)^T
+            y = Yc.t[: S * m, : c1 - c0]                         # (S m, ny_r) row-major
+            if e is not None:
+                y = y + e.reshape(S * m, 1)                      # one scalar per row
+            if not std:
+                y = blas.standardize(y.contiguous(), mu, sd, inverse=True)
         if dist_on and gather:
             counts = [gdist.shard_range(sd_.K.shape[1], r, ctx.world) for r in range(ctx.world)]
             y = gdist.gather_cols(ctx, y.contiguous(), [b - a for a, b in counts])
             if y is None:
                 return None
+        if not to_host:
+            return y.reshape(S, m, -1)
         return _to_host(y.reshape(S, m, -1), out_dtype)
 
 

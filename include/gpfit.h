@@ -422,6 +422,20 @@ int gp_standardize(const double* Y, int n, int ny, long long ldy, const double* 
                    const double* sd, double* out, long long ldo, int inverse,
                    hipStream_t stream);
 
+/* Field reconstruction, SepiaEmulatorPrediction.get_y() (time_predictions.py:79-90,
+ * assess_all_models.py:489-500) in one pass:
+ *   Y[r*ldy + c] = ((sum_j W[r*ldw + j] K[j*ldk + c]) + err[r]) * sd[c] + mu[c]
+ * for r < rows (samples x test points), c < ncols (field nodes), j < P <= gp_field_max_pcs()
+ * PCs; fp64 MFMA products, the back-transform and the optional error term (one scalar per row,
+ * err may be NULL) in the epilogue, stored once as float32 (out_f32 = 1, the reference's
+ * .w.astype(float32) path) or fp64.  sd and mu NULL together: Y = W K (+ err), the
+ * standardised field.  Equal bit for bit to gp_dgemm (K <= 64) + gp_standardize(inverse = 1)
+ * + a float32 cast.  Returns -4 for P outside [1, gp_field_max_pcs()]. */
+int gp_field_max_pcs(void);
+int gp_field(const double* W, long long ldw, int rows, int P, const double* K, long long ldk,
+             int ncols, const double* sd, const double* mu, const double* err, void* Y,
+             long long ldy, int out_f32, hipStream_t stream);
+
 /* out[0] = mean(x), out[1] = var(x, ddof) of a length-N vector (two-pass, deterministic);
  * work holds 1024 doubles.  np.var of the PC truncation residual, src/model.py:222. */
 int gp_mean_var(const double* x, long long N, int ddof, double* out, double* work,

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-6 GPU job runner: tools/gpu_r06.sh TAG STEP...  (each step under its own time limit;
+# stops at the first failing step).  Logs to gpurun_out/r06_TAG_*.
+set -o pipefail
+tag=$1; shift
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() { local name=$1 lim=$2; shift 2; echo "== $name ($(date +%T))"; timeout -k 10 "$lim" "$@" > "gpurun_out/r06_${tag}_${name}.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -3 "gpurun_out/r06_${tag}_${name}.log"; return $rc; }
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  case $step in
+    t_*) f=${step#t_}; run "$step" 600 $PYT "tests/test_gpu_${f}.py" || exit $? ;;
+    gpu) run gpu 1100 $PYT -m gpu tests || exit $? ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) run bench 400 python -u bench.py || exit $? ;;
+    c4) run c4 400 python -u bench.py --workload c4 || exit $? ;;
+    c5) run c5 400 python -u bench.py --workload c5 || exit $? ;;
+    c5q) run c5q 300 python -u bench.py --workload c5 --no-cpu --steps 5 --warmup 2 || exit $? ;;
+    fit) run fit 400 python -u bench.py --workload fit || exit $? ;;
+    prof_c5) run prof_c5 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_${tag}_prof_c5 -o c5 -- python -u bench.py --workload c5 --no-cpu --steps 5 --warmup 2 || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
