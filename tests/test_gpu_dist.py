@@ -286,3 +286,58 @@ def test_two_ranks_scalar_gp_points_sharded(tmp_path):
         res = dict(results[r])
         assert "error" not in res, res.get("error")
         assert res["shard"] == "points" and res["eq"], res
+
+
+def _c5_worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from gladsgp_amd import dist as gdist
+    from gladsgp_amd.pipeline import FieldPipeline, synthetic_c5
+    ctx = gdist.init_from_env("cuda", backend="gloo", device_index=0)
+    out = {}
+    try:
+        dev = ctx.device
+        t, Y, omega, smp, t_pred = synthetic_c5(n=96, d=5, ny=700, m=3001, p=8, samples=2,
+                                                modes=16)
+        sh = FieldPipeline(t, Y, omega, smp, t_pred, 8, device=dev, ctx=ctx)
+        rs = sh.run()
+        full = FieldPipeline(t, Y, omega, smp, t_pred, 8, device=dev)
+        rf = full.run()
+        torch.cuda.synchronize()
+        c0, c1 = rs["y_cols"]
+        out["cols"] = (c0, c1)
+        out["blk"] = bool(torch.equal(rs["y"], rf["y"][:, :, c0:c1]))
+        out["svd"] = bool(torch.equal(rs["S"], rf["S"]) and torch.equal(rs["K"], rf["K"]))
+        if rank == 0:
+            out["w"] = bool(torch.equal(rs["mean"], rf["mean"]) and
+                            torch.equal(rs["var"], rf["var"]))
+        else:
+            out["w"] = rs["mean"] is None and rs["var"] is None
+        sh.close()
+        full.close()
+    except Exception as exc:  # report, do not hang the peer
+        out["error"] = repr(exc)
+    finally:
+        results[rank] = out
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_c5_pipeline():
+    """bench --workload c5's N-rank path (gladsgp_amd.pipeline.FieldPipeline with a process
+    group): the (sample, PC) GPs dealt round-robin and gathered to rank 0 equal one process's
+    bit for bit; every rank's ny-column block of the field equals those columns of one
+    process's field bit for bit; the redundant SVD / basis is identical on both ranks."""
+    world = 2
+    port = _free_port()
+    mgr = mp.get_context("spawn").Manager()
+    results = mgr.dict()
+    mp.start_processes(_c5_worker, args=(world, port, results), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert "error" not in results[r], results[r]
+        assert results[r]["blk"] and results[r]["svd"] and results[r]["w"], results[r]
+    assert results[0]["cols"][0] == 0 and results[1]["cols"][1] == 700
+    assert results[0]["cols"][1] == results[1]["cols"][0]
