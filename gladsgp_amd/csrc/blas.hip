@@ -197,6 +197,46 @@ __global__ __launch_bounds__(256) void simstats_kernel(const double* __restrict_
   sd[c] = v;
 }
 
+// The same statistics for a short field (ny below kSimStatsSplitNy: a thread per location would
+// leave most CUs idle -- 40 blocks at C5's 10k nodes took 252 us, profiles/r06/
+// r06b_c5_kernel_stats.csv): 64 locations per block, the rows in four consecutive quarters
+// summed by four thread groups, the quarter sums added in quarter order (a fixed order:
+// deterministic), for the mean and then the centred sum of squares.
+constexpr int kSimStatsSplitNy = 1 << 16;
+__global__ __launch_bounds__(256) void simstats_split_kernel(const double* __restrict__ Y, int n,
+                                                             int ny, long long ldy,
+                                                             double sd_floor,
+                                                             double* __restrict__ mu,
+                                                             double* __restrict__ sd) {
+  __shared__ double part[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int q = (n + 3) / 4, r0 = min(n, g * q), r1 = min(n, r0 + q);
+  const double* y = Y + (c < ny ? c : 0);
+  double s = 0.0;
+  if (c < ny)
+    for (int r = r0; r < r1; ++r) s += y[(long long)r * ldy];
+  part[g][cl] = s;
+  __syncthreads();
+  const double mean = (((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl]) / n;
+  __syncthreads();
+  double t2 = 0.0;
+  if (c < ny)
+    for (int r = r0; r < r1; ++r) {
+      const double t = y[(long long)r * ldy] - mean;
+      t2 = fma(t, t, t2);
+    }
+  part[g][cl] = t2;
+  __syncthreads();
+  if (g == 0 && c < ny) {
+    const double qs = ((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl];
+    double v = sqrt(qs / (n > 1 ? n - 1 : 1));
+    if (v < sd_floor) v = sd_floor;
+    mu[c] = mean;
+    sd[c] = v;
+  }
+}
+
 // out[r*ldo + c] = (Y[r*ldy + c] - mu[c]) / sd[c]   (inverse = 0, src/model.py:72)
 // out[r*ldo + c] =  Y[r*ldy + c] * sd[c] + mu[c]    (inverse = 1, get_y's back-transform)
 __global__ void standardize_kernel(const double* __restrict__ Y, int n, int ny, long long ldy,
@@ -899,8 +939,12 @@ extern "C" int gp_sim_stats(const double* Y, int n, int ny, long long ldy, doubl
   if (!mu) return -6;
   if (!sd) return -7;
   if (ny == 0) return 0;
-  hipLaunchKernelGGL(simstats_kernel, dim3(gp_ceil_div(ny, 256)), dim3(256), 0, stream, Y, n, ny,
-                     ldy, sd_floor, mu, sd);
+  if (ny < kSimStatsSplitNy)
+    hipLaunchKernelGGL(simstats_split_kernel, dim3(gp_ceil_div(ny, 64)), dim3(256), 0, stream, Y,
+                       n, ny, ldy, sd_floor, mu, sd);
+  else
+    hipLaunchKernelGGL(simstats_kernel, dim3(gp_ceil_div(ny, 256)), dim3(256), 0, stream, Y, n,
+                       ny, ldy, sd_floor, mu, sd);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }

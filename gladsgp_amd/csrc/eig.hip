@@ -16,26 +16,34 @@
 namespace {
 
 constexpr int kMaxR = 1024;   // LDS: rotations + pairing + sort keys, ~30 KB
+// r <= kLdsR: A and V live in LDS for the whole solve (2 x 64 x 65 doubles): a global round
+// trip per phase (3 per round, 63 rounds per sweep at r = 64) made the L2-resident form take
+// 3.35 ms for the C5 basis's 64 x 64 B B^T (profiles/r06/r06b_c5_kernel_stats.csv)
+constexpr int kLdsR = 64;
+constexpr int kLdsPitch = kLdsR + 1;
 
-__global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int r, int lda,
-                                                     double* __restrict__ W,
-                                                     double* __restrict__ V, int ldv,
-                                                     int max_sweeps, double tol,
-                                                     int* __restrict__ sweeps_out,
-                                                     int want_sqrt) {
-  __shared__ double cs[kMaxR / 2], sn[kMaxR / 2];
-  __shared__ int pp[kMaxR / 2], qq[kMaxR / 2];
-  __shared__ double red[17];
-  __shared__ int perm[kMaxR];
-  __shared__ double ws[kMaxR];
-  __shared__ int done;
+// column-major r x r matrix views: global (leading dimension) or LDS (fixed pitch)
+struct GMat {
+  double* p;
+  int ld;
+  GP_DEV double& operator()(int i, int j) const { return p[i + (long long)j * ld]; }
+};
+struct LMat {
+  double* p;
+  GP_DEV double& operator()(int i, int j) const { return p[i + j * kLdsPitch]; }
+};
+
+// The cyclic Jacobi sweep loop and the descending sort, on views A and V (the same operations
+// in the same order whichever memory holds them: bit-identical results).
+template <typename MA, typename MV>
+GP_DEV int syevj_solve(MA A, MV V, int r, int max_sweeps, double tol, double* cs, double* sn,
+                       int* pp, int* qq, double* red, int* done) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int R = (r + 1) & ~1;          // padded to even; index r (if any) is a dummy
   const int npair = R / 2;
-  // V = I
   for (int g = tid; g < r * r; g += nt) {
     const int i = g % r, j = g / r;
-    V[i + (long long)j * ldv] = (i == j) ? 1.0 : 0.0;
+    V(i, j) = (i == j) ? 1.0 : 0.0;
   }
   __syncthreads();
   int sweep = 0;
@@ -44,7 +52,7 @@ __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int
     double off = 0.0, tot = 0.0;
     for (int g = tid; g < r * r; g += nt) {
       const int i = g % r, j = g / r;
-      const double a = A[i + (long long)j * lda];
+      const double a = A(i, j);
       tot += a * a;
       if (i != j) off += a * a;
     }
@@ -68,10 +76,10 @@ __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int
     if (tid == 0) {
       double st = 0.0;
       for (int q = 0; q < (nt + 63) / 64; ++q) st += red[q];
-      done = (offs <= tol * tol * st) ? 1 : 0;
+      *done = (offs <= tol * tol * st) ? 1 : 0;
     }
     __syncthreads();
-    if (done) break;
+    if (*done) break;
     for (int round = 0; round < R - 1; ++round) {
       // round-robin pairing: position 0 fixed, positions 1..R-1 rotate
       if (tid < npair) {
@@ -81,9 +89,9 @@ __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int
         if (p > q) { const int t = p; p = q; q = t; }
         double c = 1.0, s = 0.0;
         if (q < r) {
-          const double apq = A[p + (long long)q * lda];
+          const double apq = A(p, q);
           if (apq != 0.0) {
-            const double app = A[p + (long long)p * lda], aqq = A[q + (long long)q * lda];
+            const double app = A(p, p), aqq = A(q, q);
             const double theta = (aqq - app) / (2.0 * apq);
             const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(1.0 + theta * theta));
             c = 1.0 / sqrt(1.0 + t * t);
@@ -102,11 +110,9 @@ __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int
         const int p = pp[t], q = qq[t];
         if (q >= r) continue;
         const double c = cs[t], s = sn[t];
-        double* ap = A + p + (long long)k * lda;
-        double* aq = A + q + (long long)k * lda;
-        const double x = *ap, y = *aq;
-        *ap = c * x - s * y;
-        *aq = s * x + c * y;
+        const double x = A(p, k), y = A(q, k);
+        A(p, k) = c * x - s * y;
+        A(q, k) = s * x + c * y;
       }
       __syncthreads();
       // phase 2: columns p, q of A (A <- A J) and of V (V <- V J)
@@ -115,23 +121,27 @@ __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int
         const int p = pp[t], q = qq[t];
         if (q >= r) continue;
         const double c = cs[t], s = sn[t];
-        double* ap = A + k + (long long)p * lda;
-        double* aq = A + k + (long long)q * lda;
-        double x = *ap, y = *aq;
-        *ap = c * x - s * y;
-        *aq = s * x + c * y;
-        double* vp = V + k + (long long)p * ldv;
-        double* vq = V + k + (long long)q * ldv;
-        x = *vp;
-        y = *vq;
-        *vp = c * x - s * y;
-        *vq = s * x + c * y;
+        double x = A(k, p), y = A(k, q);
+        A(k, p) = c * x - s * y;
+        A(k, q) = s * x + c * y;
+        x = V(k, p);
+        y = V(k, q);
+        V(k, p) = c * x - s * y;
+        V(k, q) = s * x + c * y;
       }
       __syncthreads();
     }
   }
-  // sort eigenvalues descending; permute V's columns (stable selection by one thread)
-  if (tid < r) ws[tid] = A[tid + (long long)tid * lda];
+  return sweep;
+}
+
+// sort eigenvalues descending (stable selection by one thread), W = eigenvalues or their square
+// roots, the columns of V permuted to match and written to Vout (via the scratch view T)
+template <typename MA, typename MV>
+GP_DEV void syevj_finish(MA A, MV V, int r, int sweep, double* W, GMat Vout, int* perm,
+                         double* ws, int* sweeps_out, int want_sqrt) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid < r) ws[tid] = A(tid, tid);
   __syncthreads();
   if (tid == 0) {
     for (int i = 0; i < r; ++i) perm[i] = i;
@@ -148,15 +158,62 @@ __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int
     const double ev = ws[perm[tid]];
     W[tid] = want_sqrt ? sqrt(ev > 0.0 ? ev : 0.0) : ev;   // singular values of B when A = B B^T
   }
-  // permuted copy of V into A's storage, then back (A is scratch now)
+  // permuted copy of V into A's storage, then out (A is scratch now)
   for (int g = tid; g < r * r; g += nt) {
     const int i = g % r, j = g / r;
-    A[i + (long long)j * lda] = V[i + (long long)perm[j] * ldv];
+    A(i, j) = V(i, perm[j]);
   }
   __syncthreads();
   for (int g = tid; g < r * r; g += nt) {
     const int i = g % r, j = g / r;
-    V[i + (long long)j * ldv] = A[i + (long long)j * lda];
+    Vout(i, j) = A(i, j);
+  }
+}
+
+__global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int r, int lda,
+                                                     double* __restrict__ W,
+                                                     double* __restrict__ V, int ldv,
+                                                     int max_sweeps, double tol,
+                                                     int* __restrict__ sweeps_out,
+                                                     int want_sqrt) {
+  __shared__ double cs[kMaxR / 2], sn[kMaxR / 2];
+  __shared__ int pp[kMaxR / 2], qq[kMaxR / 2];
+  __shared__ double red[17];
+  __shared__ int perm[kMaxR];
+  __shared__ double ws[kMaxR];
+  __shared__ int done;
+  const GMat Ag{A, lda}, Vg{V, ldv};
+  const int sweep = syevj_solve(Ag, Vg, r, max_sweeps, tol, cs, sn, pp, qq, red, &done);
+  syevj_finish(Ag, Vg, r, sweep, W, Vg, perm, ws, sweeps_out, want_sqrt);
+}
+
+// r <= kLdsR: the same solve on LDS copies of A and V; A (global) is left holding the
+// eigenvalue-sorted V, as the global form leaves it
+__global__ __launch_bounds__(1024) void syevj_lds_kernel(double* __restrict__ A, int r, int lda,
+                                                         double* __restrict__ W,
+                                                         double* __restrict__ V, int ldv,
+                                                         int max_sweeps, double tol,
+                                                         int* __restrict__ sweeps_out,
+                                                         int want_sqrt) {
+  __shared__ double al[kLdsR * kLdsPitch], vl[kLdsR * kLdsPitch];
+  __shared__ double cs[kLdsR / 2], sn[kLdsR / 2];
+  __shared__ int pp[kLdsR / 2], qq[kLdsR / 2];
+  __shared__ double red[17];
+  __shared__ int perm[kLdsR];
+  __shared__ double ws[kLdsR];
+  __shared__ int done;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const LMat Al{al}, Vl{vl};
+  for (int g = tid; g < r * r; g += nt) {
+    const int i = g % r, j = g / r;
+    Al(i, j) = A[i + (long long)j * lda];
+  }
+  __syncthreads();
+  const int sweep = syevj_solve(Al, Vl, r, max_sweeps, tol, cs, sn, pp, qq, red, &done);
+  syevj_finish(Al, Vl, r, sweep, W, GMat{V, ldv}, perm, ws, sweeps_out, want_sqrt);
+  for (int g = tid; g < r * r; g += nt) {
+    const int i = g % r, j = g / r;
+    A[i + (long long)j * lda] = Al(i, j);
   }
 }
 
@@ -173,8 +230,12 @@ extern "C" int gp_syevj(double* A, int r, int lda, double* W, double* V, int ldv
   if (ldv < r || ldv < 1) return -6;
   if (max_sweeps < 0) return -7;
   if (r == 0) return 0;
-  hipLaunchKernelGGL(syevj_kernel, dim3(1), dim3(1024), 0, stream, A, r, lda, W, V, ldv,
-                     max_sweeps, tol, sweeps, want_sqrt);
+  if (r <= kLdsR)
+    hipLaunchKernelGGL(syevj_lds_kernel, dim3(1), dim3(1024), 0, stream, A, r, lda, W, V, ldv,
+                       max_sweeps, tol, sweeps, want_sqrt);
+  else
+    hipLaunchKernelGGL(syevj_kernel, dim3(1), dim3(1024), 0, stream, A, r, lda, W, V, ldv,
+                       max_sweeps, tol, sweeps, want_sqrt);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
 }

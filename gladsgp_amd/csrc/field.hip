@@ -29,7 +29,18 @@ namespace {
 
 // rows of w per tile: 32 (two 16-row MFMA sub-tiles) while the K panel leaves room for their
 // accumulators, 16 at P > 32 (K panel 128 + accumulators 32 of 256 registers at P = 64)
-template <int KS> constexpr int field_rows() { return KS <= 8 ? 32 : 16; }
+#ifndef FIELD_ROWS_BIG
+#define FIELD_ROWS_BIG 16
+#endif
+#ifndef FIELD_OCC
+#define FIELD_OCC 2
+#endif
+// non-temporal output stores (the field is written once and not re-read by this kernel):
+// 3.26 vs 3.78 ms at C5 (profiles/r06/r06c_field_ab.log), same bits
+#ifndef FIELD_NT
+#define FIELD_NT 1
+#endif
+template <int KS> constexpr int field_rows() { return KS <= 8 ? 32 : FIELD_ROWS_BIG; }
 constexpr int kFieldCols = 256;              // output columns per block (64 per wave)
 constexpr int kFieldPitch = 68;              // LDS row pitch of a w tile (doubles)
 constexpr int kFieldMaxP = 64;
@@ -39,7 +50,7 @@ constexpr int kFieldMaxP = 64;
 // U = npanels x ntiles (one residency round of B blocks: no tail round), reloading its K panel
 // when its range crosses into the next panel.
 template <int KS, bool F32>
-__global__ __launch_bounds__(256, 2) void field_kernel(const double* __restrict__ W,
+__global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __restrict__ W,
                                                        long long ldw, int rows, int P,
                                                        const double* __restrict__ K,
                                                        long long ldk, int ncols,
@@ -93,15 +104,16 @@ __global__ __launch_bounds__(256, 2) void field_kernel(const double* __restrict_
     }
   };
 
-  load_tile(u0 % ntiles);
+  long long panel = u0 / ntiles, t = u0 - panel * ntiles;  // unit u = panel * ntiles + t
+  load_tile(t);
   store_tile(0);
   __syncthreads();
   int buf = 0;
   for (long long u = u0; u < u1; ++u) {
-    const long long panel = u / ntiles, t = u - panel * ntiles;
     if (panel != cur) load_panel(panel);
     const bool more = u + 1 < u1;
-    if (more) load_tile((u + 1) % ntiles);               // in flight under the MFMAs
+    const long long tn = t + 1 == ntiles ? 0 : t + 1;
+    if (more) load_tile(tn);                             // in flight under the MFMAs
     f64x4 acc[RS][4];
 #pragma unroll
     for (int rs = 0; rs < RS; ++rs)
@@ -144,10 +156,15 @@ __global__ __launch_bounds__(256, 2) void field_kernel(const double* __restrict_
           double v = acc[rs][jt][q];
           if (err) v = v + e;
           if (sd) v = fma(v, s_c[jt], m_c[jt]);
-          if constexpr (F32)
-            static_cast<float*>(Y)[r * ldy + c] = static_cast<float>(v);
-          else
-            static_cast<double*>(Y)[r * ldy + c] = v;
+          if constexpr (F32) {
+            float* yp = static_cast<float*>(Y) + r * ldy + c;
+            if constexpr (FIELD_NT) __builtin_nontemporal_store(static_cast<float>(v), yp);
+            else *yp = static_cast<float>(v);
+          } else {
+            double* yp = static_cast<double*>(Y) + r * ldy + c;
+            if constexpr (FIELD_NT) __builtin_nontemporal_store(v, yp);
+            else *yp = v;
+          }
         }
       }
     if (more) {
@@ -155,6 +172,8 @@ __global__ __launch_bounds__(256, 2) void field_kernel(const double* __restrict_
       __syncthreads();
       buf ^= 1;
     }
+    if (tn == 0) ++panel;
+    t = tn;
   }
 }
 
@@ -177,7 +196,7 @@ hipError_t launch_field(const double* W, long long ldw, int rows, int P, const d
   const long long npanels = gp_ceil_div(ncols, kFieldCols);
   constexpr int kFieldRows = field_rows<KS>();
   const long long ntiles = ((long long)rows + kFieldRows - 1) / kFieldRows;
-  long long blocks = 2LL * field_num_cus();              // one residency round
+  long long blocks = (long long)FIELD_OCC * field_num_cus();   // one residency round
   if (blocks > npanels * ntiles) blocks = npanels * ntiles;
   hipLaunchKernelGGL((field_kernel<KS, F32>), dim3((unsigned)blocks), dim3(256), 0, stream, W,
                      ldw, rows, P, K, ldk, ncols, sd, mu, err, Y, ldy, ntiles);

@@ -19,6 +19,9 @@ for step in "$@"; do
     c5q) run c5q 300 python -u bench.py --workload c5 --no-cpu --steps 5 --warmup 2 || exit $? ;;
     fit) run fit 400 python -u bench.py --workload fit || exit $? ;;
     prof_c5) run prof_c5 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_${tag}_prof_c5 -o c5 -- python -u bench.py --workload c5 --no-cpu --steps 5 --warmup 2 || exit $? ;;
+    field_ab) run field_ab 300 python -u tools/field_ab.py || exit $? ;;
+    c4q) run c4q 300 python -u bench.py --workload c4 --no-cpu --steps 5 --warmup 2 || exit $? ;;
+    c3q) run c3q 300 python -u bench.py --no-cpu --steps 10 --warmup 3 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
