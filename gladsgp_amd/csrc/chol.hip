@@ -199,6 +199,10 @@ __shared__ Smem g_sm;
 // chain: L_j+1,j as [p][r] (opA layout) between steps, the two-wave leaf's multipliers during
 // the diagonal factor; workers: the XT pair's third tile
 __shared__ double g_keep[NB * LP];
+// gp_loglik in-chain mode only (referenced by pp_kernel<true> alone): [0, 64) z_{j-1} (chain)
+// or the current term's z_k (DP task), [64, 128) y_j, [128, 384) four 64-row partial sums
+__shared__ double g_ll[6 * NB];
+constexpr int kLLZ = 0, kLLY = NB, kLLPart = 2 * NB;
 using lds_double = __attribute__((address_space(3))) double;
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 using lds_dvec2 = __attribute__((address_space(3))) const dvec2;
@@ -1102,6 +1106,13 @@ struct PPArgs {
   int* head;                          // [0] dequeue counter, [1] workgroups that have left,
                                       // [32 + 4g] group g's dequeue counter
   int* flags; int fstride;            // per problem: FL[N*N], FX[N*N], DPF[N], SPF[N], abort
+  // gp_loglik's in-chain mode (pp_kernel<true>, inv = 0): the right-hand sides w (problem b at
+  // w + b ldw), the forward-substitution scratch zb (problem b at zb + b zld: z_j at j 64,
+  // DP(j)'s partial sums zq_j at zq_off + j 64), per problem sum z^2 (zz), and the outputs
+  // ll / status / info_out of gp_loglik.  FZ[j] (z_j stored) lives in the unused FX flags.
+  const double* w; int ldw;
+  double* zb; int zld, zq_off;
+  double* zz; double* ll; int* status; int* info_out;
 #ifdef GPFIT_PP_TRACE
   int* dbg;                           // trace build only: per-workgroup progress words
   long long* trace;                   // trace build only: per-task / per-chain-step stamps
@@ -1346,6 +1357,7 @@ struct PPTask {
   int kind, b, i, j, nterms, idx;
 };
 
+template <bool LL>
 GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
   const int N = P.N;
   double* Ab = P.A + T.b * P.sA;
@@ -1374,6 +1386,7 @@ GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
   } else if (T.kind == kTDP) {             // L_jk L_jk^T
     u.a = atile(T.j, t);  u.fa = F + T.j * N + t;  u.av = rv(T.j);  u.ca = hz(T.j, t);
     u.b = u.a;            u.fb = u.fa;             u.bv = u.av;     u.cb = u.ca;
+    if constexpr (LL) u.fc = F + N * N + t;  // (+ L_jk z_k: z_k stored by chain step k, FZ[k])
   } else {                                 // XT: L_ik X_kc, k = c + t (X_cc = D_c)
     const int k = T.j + t;
     u.a = atile(T.i, k);  u.fa = F + T.i * N + k;  u.av = rv(T.i);  u.ca = hz(T.i, k);
@@ -1396,6 +1409,7 @@ GP_DEV PPTerm pp_term(const PPArgs& P, const PPTask& T, int t) {
 
 // Lane-parallel readiness scan: the number of consecutive terms t0, t0+1, ... whose input
 // flags are all set (wave 0, one term per lane), at least 1 unless the problem aborted (-1).
+template <bool LL>
 GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -1405,7 +1419,7 @@ GP_DEV int pp_ready(const PPArgs& P, const PPTask& T, int t0, int* abort) {
       const int t = t0 + lane;
       bool rdy = true;
       if (t < T.nterms) {
-        const PPTerm u = pp_term(P, T, t);
+        const PPTerm u = pp_term<LL>(P, T, t);
         rdy = pp_ldflag(u.fa) != 0 && pp_ldflag(u.fb) != 0 && (!u.fc || pp_ldflag(u.fc) != 0);
       }
       const unsigned long long m = __ballot(rdy);
@@ -1436,8 +1450,12 @@ GP_DEV void pp_load_term(const PPTerm& u, OpTile& ta, OpTile& tb, OpTile& tc) {
 // The paired XT2 accumulates its second output in acc2 from the third tile (staged in g_keep,
 // which only the chain uses otherwise): acc2 += L_ik X_k,c+1, sharing opA: three tile loads
 // per two tile-terms instead of four.
+// LL (gp_loglik's in-chain mode) DP tasks also accumulate zq = sum_k L_jk z_k (this thread: row
+// tid & 63, columns 16 (tid >> 6) .. + 15 of each term, k ascending) from the term's tile in LDS
+// and z_k (staged in g_ll by the first wave with the tile; its flag FZ[k] is one of the term's).
+template <bool LL>
 GP_DEV bool pp_accumulate(const PPArgs& P, const PPTask& T, f64x4 (&acc)[2][2],
-                          f64x4 (&acc2)[2][2], int* abort) {
+                          f64x4 (&acc2)[2][2], int* abort, double& zq) {
   Smem& sm = g_sm;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -1446,12 +1464,21 @@ GP_DEV bool pp_accumulate(const PPArgs& P, const PPTask& T, f64x4 (&acc)[2][2],
       acc[mi][nj] = zero4();
       acc2[mi][nj] = zero4();
     }
+  zq = 0.0;
   if (T.nterms == 0) return true;
+  const bool lldp = LL && T.kind == kTDP;
+  double zr = 0.0;                                   // z_k of the term in flight (tid < 64)
+  auto ldz = [&](int t) {
+    if (lldp && threadIdx.x < 64)
+      zr = __hip_atomic_load(P.zb + (long long)T.b * P.zld + t * NB + threadIdx.x,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   OpTile ta, tb, tc;
-  int avail = pp_ready(P, T, 0, abort);      // terms [0, avail) are ready
+  int avail = pp_ready<LL>(P, T, 0, abort);  // terms [0, avail) are ready
   if (avail < 0) return false;
-  PPTerm u = pp_term(P, T, 0);
+  PPTerm u = pp_term<LL>(P, T, 0);
   pp_load_term(u, ta, tb, tc);
+  ldz(0);
   for (int t = 0; t < T.nterms; ++t) {
     const bool same = u.b == u.a;
     const bool trn = u.btrn;
@@ -1463,21 +1490,29 @@ GP_DEV bool pp_accumulate(const PPArgs& P, const PPTask& T, f64x4 (&acc)[2][2],
       else store_op<false>(sm.Bs, tb);
     }
     if (third) store_op<true>(g_keep, tc);
+    if (lldp && threadIdx.x < 64) g_ll[kLLZ + threadIdx.x] = zr;
     __syncthreads();
     const bool more = t + 1 < T.nterms;
     const bool pre = more && t + 1 < avail;
     if (pre) {
-      u = pp_term(P, T, t + 1);
+      u = pp_term<LL>(P, T, t + 1);
       pp_load_term(u, ta, tb, tc);
+      ldz(t + 1);
     }
     mma64_add(sm.As, same ? sm.As : sm.Bs, acc);
     if (third) mma64_add(sm.As, g_keep, acc2);
+    if (lldp) {
+      const int r = threadIdx.x & 63, c0 = 16 * (threadIdx.x >> 6);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) zq = fma(sm.As[(c0 + c) * LP + r], g_ll[kLLZ + c0 + c], zq);
+    }
     if (more && !pre) {
-      const int r = pp_ready(P, T, t + 1, abort);
+      const int r = pp_ready<LL>(P, T, t + 1, abort);
       if (r < 0) return false;
       avail = t + 1 + r;
-      u = pp_term(P, T, t + 1);
+      u = pp_term<LL>(P, T, t + 1);
       pp_load_term(u, ta, tb, tc);
+      ldz(t + 1);
     }
   }
   return true;
@@ -1532,6 +1567,7 @@ GP_DEV double* pp_dptr(const PPArgs& P, int b, int j, int& ld) {
 #define PP_TASK GP_DEV
 #endif
 
+template <bool LL>
 PP_TASK void pp_worker(const PPArgs& P, const PPTask& T) {
   Smem& sm = g_sm;
   const int N = P.N;
@@ -1557,7 +1593,8 @@ PP_TASK void pp_worker(const PPArgs& P, const PPTask& T) {
   const int ar = T.kind == kTDP ? T.j : (T.kind == kTSP ? T.j + 1 : T.i);
   OpTile ta;
   if (!xt) pp_load(ta, atile(ar, T.j), P.lda, rv(ar), T.kind == kTL ? NB : rv(T.j));
-  if (!pp_accumulate(P, T, acc, acc2, abort)) return;
+  double zq;
+  if (!pp_accumulate<LL>(P, T, acc, acc2, abort, zq)) return;
   PP_MARK(P, 30 + T.kind, T.i * 1000 + T.j);
   PP_TRACE(P, tr + 2, pp_now());
   // slot 0: workgroup | ticks polled before the K loop finished << 8
@@ -1568,6 +1605,20 @@ PP_TASK void pp_worker(const PPArgs& P, const PPTask& T) {
     double* dst = atile(r, T.j);
     pp_sub_tile(ta, rv(r), rv(T.j), T.kind == kTDP, acc);
     pp_store_cm(dst, P.lda, sm.As, rv(r), rv(T.j), false, T.kind == kTDP);
+    if constexpr (LL) {
+      if (T.kind == kTDP) {
+        // zq_j = sum_{k < j-1} L_jk z_k for the chain's y_j: the four column quarters' partial
+        // sums added in quarter order (a fixed order)
+        g_ll[kLLPart + threadIdx.x] = zq;
+        __syncthreads();
+        if (threadIdx.x < 64 && threadIdx.x < rv(T.j)) {
+          const double* pq = g_ll + kLLPart + threadIdx.x;
+          __hip_atomic_store(P.zb + (long long)T.b * P.zld + P.zq_off + T.j * NB + threadIdx.x,
+                             ((pq[0] + pq[64]) + pq[128]) + pq[192], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
     pp_publish(T.kind == kTDP ? F + 2 * N * N + T.j : F + 2 * N * N + N + T.j);
     PP_TRACE(P, tr + 3, pp_now());
     return;
@@ -1628,6 +1679,33 @@ PP_TASK void pp_worker(const PPArgs& P, const PPTask& T) {
 }
 
 // The chain of problem b (see the section comment).
+// gp_loglik's in-chain mode: z_j = D_j y_j (y_j = w_j - zq_j - L_j,j-1 z_j-1 in g_ll, D_j in
+// sm.Bs as [row][col]) into g_ll's z slot and the problem's z scratch; sum z^2 accumulated in
+// order on thread 0.  The four column quarters' partial sums are added in quarter order.
+GP_DEV void ll_zstep(const PPArgs& P, int b, int j, int nb, double& zz) {
+  Smem& sm = g_sm;
+  const int r = threadIdx.x & 63, c0 = 16 * (threadIdx.x >> 6);
+  double part = 0.0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) part = fma(sm.Bs[r * LP + c0 + c], g_ll[kLLY + c0 + c], part);
+  g_ll[kLLPart + threadIdx.x] = part;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const double* pq = g_ll + kLLPart + r;
+    const double z = r < nb ? ((pq[0] + pq[64]) + pq[128]) + pq[192] : 0.0;
+    g_ll[kLLZ + r] = z;
+    if (r < nb)
+      __hip_atomic_store(P.zb + (long long)b * P.zld + j * NB + r, z, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    double q = z * z;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
+    if (r == 0) zz += q;
+  }
+  __syncthreads();
+}
+
+template <bool LL>
 PP_TASK void pp_chain(const PPArgs& P, int b) {
   Smem& sm = g_sm;
   const int N = P.N;
@@ -1636,6 +1714,7 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
   double* Ab = P.A + b * P.sA;
   auto atile = [&](int r, int c) { return Ab + r * NB + (long long)c * NB * P.lda; };
   double ld_sum = 0.0;
+  double zz = 0.0;           // (LL) sum of z^2 so far (thread 0)
   OpTile tpj;                // P_jj, loaded by the previous step when its partials were ready
   bool pref = false;
   // L_j,j-1 L_j,j-1^T for step j, computed at the end of step j-1 while that step's stores
@@ -1661,6 +1740,16 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
       if (j >= 2 && !pp_wait1(F + 2 * N * N + j, abort, P.budget)) return;
       pp_load(tpj, atile(j, j), P.lda, nb, nb);
     }
+    // (LL) this step's right-hand side w_j and DP(j)'s partial sum zq_j (its flag is set here)
+    double wq = 0.0;
+    if constexpr (LL) {
+      if (threadIdx.x < 64 && threadIdx.x < nb) {
+        wq = P.w[(long long)b * P.ldw + j * NB + threadIdx.x];
+        if (j >= 2)
+          wq -= __hip_atomic_load(P.zb + (long long)b * P.zld + P.zq_off + j * NB + threadIdx.x,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     PP_TRACE(P, tb0 + 1, pp_now());
     __syncthreads();
     store_op<false>(sm.Bs, tpj);                        // Bs[c][r] = P(r, c) (r >= c valid)
@@ -1678,6 +1767,23 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
           sm.As[row * LP + col] = v;
         }
     __syncthreads();
+    if constexpr (LL) {
+      // y_j = (w_j - zq_j) - L_j,j-1 z_j-1 (L_j,j-1 in g_keep as [col][row] since step j-1)
+      const int r = threadIdx.x & 63, c0 = 16 * (threadIdx.x >> 6);
+      double part = 0.0;
+      if (j >= 1) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          part = fma(g_keep[(c0 + c) * LP + r], g_ll[kLLZ + c0 + c], part);
+      }
+      g_ll[kLLPart + threadIdx.x] = part;
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        const double* pq = g_ll + kLLPart + r;
+        g_ll[kLLY + r] = r < nb ? wq - (((pq[0] + pq[64]) + pq[128]) + pq[192]) : 0.0;
+      }
+      // (read after diag_factor_blk's barriers)
+    }
     // (b) factor + invert
     PP_MARK(P, 11, j);
     PP_TRACE(P, tb0 + 2, pp_now());
@@ -1699,6 +1805,7 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
       // last step: D_j -> X_jj (or the D scratch), L_jj -> A (lower, LAPACK layout)
       pp_store_rm(D, ldd, sm.Bs, nb, false, true);
       pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);
+      if constexpr (LL) ll_zstep(P, b, j, nb, zz);
       pp_publish(F + j * N + j);
       PP_TRACE(P, tb0 + 4, pp_now());
       break;
@@ -1739,19 +1846,29 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
     __syncthreads();
     PP_TRACE(P, tb0 + 6, pp_now());
     pp_store_cm(atile(j + 1, j), P.lda, g_keep, nb1, NB, false);
+    // (LL) z_j = D_j y_j (D_j is still in Bs), stored with L_j+1,j
+    if constexpr (LL) ll_zstep(P, b, j, nb, zz);
     // the next step's SYRK runs while L_j+1,j's stores drain, then its flag goes up
     mma64(g_keep, g_keep, syrk);
     pp_publish(F + (j + 1) * N + j);
+    if constexpr (LL)
+      if (threadIdx.x == 0) pp_stflag(F + N * N + j, 1);    // FZ[j]: z_j drained with the above
     PP_MARK(P, 15, j);
     PP_TRACE(P, tb0 + 7, pp_now());
   }
   if (threadIdx.x == 0 && P.logdet) P.logdet[b] = ld_sum;
+  if constexpr (LL)
+    if (threadIdx.x == 0) P.zz[b] = zz;
 }
 
 // The last workgroup to leave the launch (every task, chain and XT alike, has returned by then)
 // reports a poll budget spent anywhere in problem b (abort word 2) as info[b] = -1: an internal
 // error, never a pivot.  The acq_rel exit count orders every workgroup's abort / info stores
 // before the reading workgroup's loads.
+// In gp_loglik's in-chain mode it then writes every problem's log-likelihood, as
+// nll_reduce_kernel does for the L^-1 path: -(1/2 sum z^2 + 1/2 logdet), -inf for a non-PD
+// pivot (info > 0), NaN plus the sticky status word for an internal error (info = -1).
+template <bool LL>
 GP_DEV void pp_exit(const PPArgs& P) {
   if (threadIdx.x != 0) return;
   const int done = __hip_atomic_fetch_add(P.head + 1, 1, __ATOMIC_ACQ_REL,
@@ -1760,6 +1877,14 @@ GP_DEV void pp_exit(const PPArgs& P) {
   for (int b = 0; b < P.batch; ++b) {
     const int* ab = P.flags + (long long)b * P.fstride + 2 * P.N * P.N + 2 * P.N;
     if (pp_ldflag(ab) == 2) P.info[b] = -1;
+    if constexpr (LL) {
+      const int f = P.info[b];
+      const double v = 0.5 * P.zz[b] + 0.5 * P.logdet[b];
+      P.ll[b] = f < 0 ? __builtin_nan("") : -(f > 0 ? __builtin_huge_val() : v);
+      if (P.info_out) P.info_out[b] = f;
+      if (f < 0 && P.status)
+        __hip_atomic_fetch_or(P.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1782,6 +1907,7 @@ GP_DEV void pp_zero(const PPArgs& P, const PPTask& T) {
   }
 }
 
+template <bool LL>
 __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
   // per-XCD queues: workgroup w takes group w % 8's tasks, the global tasks 8k + g (pp_groups)
   const int g = (int)blockIdx.x % P.groups;
@@ -1798,7 +1924,7 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
 #endif
     if (t >= P.ntasks) {
       PP_MARK(P, 99, 0);
-      pp_exit(P);
+      pp_exit<LL>(P);
       return;
     }
     const int2 e = P.tasks[t];
@@ -1808,7 +1934,7 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
     T.i = e.y & 0xffff;
     T.j = e.y >> 16;
     if (T.kind == kTChain) {
-      pp_chain(P, T.b);
+      pp_chain<LL>(P, T.b);
       __syncthreads();
       continue;
     }
@@ -1824,7 +1950,7 @@ __global__ __launch_bounds__(256, 1) void pp_kernel(PPArgs P) {
       continue;
     }
     T.nterms = T.kind == kTL ? T.j : T.kind == kTDP ? T.j - 1 : T.kind == kTSP ? T.j : T.i - T.j;
-    pp_worker(P, T);
+    pp_worker<LL>(P, T);
   }
 }
 
@@ -2041,7 +2167,7 @@ static int num_cus() {
 static int pp_resident(hipStream_t stream) {
   static const int occ = [] {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, pp_kernel, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, pp_kernel<false>, 256, 0) != hipSuccess ||
         o <= 0)
       o = 1;
     return o;
@@ -2112,10 +2238,17 @@ static bool pp_eligible(int n, int batch, int resident) {
 // (pp_scratch bytes, 256-B aligned): one schedule launch, one persistent launch with one
 // workgroup per resident slot.  X is L^-1 (inv, zeroed by the caller) or the 64 x 64N D_k
 // scratch (ldx = 64).
+// gp_loglik's in-chain mode (gpfit_potrf_loglik): pp_kernel<true> with these PPArgs fields
+struct PPLL {
+  const double* w; int ldw;
+  double* zb; int zld, zq_off;
+  double* zz; double* ll; int* status; int* info_out;
+};
+
 static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx, long long sX,
                      int batch, int* info, double* logdet, bool inv, char* scr, int resident,
                      hipStream_t stream, GpfitPre pre = GpfitPre(),
-                     hipEvent_t ev_launch = nullptr) {
+                     hipEvent_t ev_launch = nullptr, const PPLL* ll = nullptr) {
   const int N = gp_ceil_div(n, NB);
   const PPScratch s = pp_scratch(n, batch, inv);
   const int grid = (int)(s.ntasks < resident ? s.ntasks : resident);
@@ -2151,7 +2284,15 @@ static int pp_factor(double* A, int n, int lda, long long sA, double* X, int ldx
   P.dbg = g_trace_dbg;
   P.trace = g_trace_buf;
 #endif
-  hipLaunchKernelGGL(pp_kernel, dim3(grid), dim3(256), 0, stream, P);
+  P.w = nullptr; P.ldw = 0; P.zb = nullptr; P.zld = 0; P.zq_off = 0;
+  P.zz = nullptr; P.ll = nullptr; P.status = nullptr; P.info_out = nullptr;
+  if (ll) {
+    P.w = ll->w; P.ldw = ll->ldw; P.zb = ll->zb; P.zld = ll->zld; P.zq_off = ll->zq_off;
+    P.zz = ll->zz; P.ll = ll->ll; P.status = ll->status; P.info_out = ll->info_out;
+    hipLaunchKernelGGL(pp_kernel<true>, dim3(grid), dim3(256), 0, stream, P);
+  } else {
+    hipLaunchKernelGGL(pp_kernel<false>, dim3(grid), dim3(256), 0, stream, P);
+  }
   GP_CK(hipGetLastError());
   return 0;
 }
@@ -2253,6 +2394,31 @@ int gpfit_potrf_inv_event(double* A, int n, int lda, long long strideA, double* 
     rc = potrf_sweep<kPotrfInv>(A, n, lda, strideA, Linv, ldinv, strideInv, batch, info, logdet,
                                 stream, k_ev, ev);
   }
+  gpfit_prof_end(GP_PROF_POTRF, stream);
+  return rc;
+}
+
+// gp_loglik on the persistent kernel's in-chain mode (gpfit_internal.h).
+long long gpfit_potrf_loglik_ws_bytes(int n, int batch) {
+  return (long long)pp_scratch(n, batch, false).bytes();
+}
+
+int gpfit_potrf_loglik(double* G, int n, long long strideG, double* D, long long strideD,
+                       const double* w, int ldw, double* zb, int zld, double* zz, int batch,
+                       int* info, double* logdet, double* ll, int* status, int* info_out,
+                       void* ws, long long ws_bytes, hipStream_t stream, GpfitPre pre) {
+  const int resident = pp_resident(stream);
+  if (!pp_eligible(n, batch, resident)) return 1;   // the caller's L^-1 path
+  if (!ws || !ws_aligned(ws)) return -11;
+  if (ws_bytes < gpfit_potrf_loglik_ws_bytes(n, batch)) return -12;
+  const int N = gp_ceil_div(n, NB);
+  if (strideD < (long long)NB * NB * N || zld < 2 * NB * N) return -13;
+  PPLL L{w, ldw, zb, zld, NB * N, zz, ll, status, info_out};
+  // (the profiler's POTRF pair brackets the Gram `pre` too on this path: it is enqueued
+  // between the schedule kernel and pp_kernel; the fit's roofline subtracts nothing for it)
+  gpfit_prof_begin(GP_PROF_POTRF, stream);
+  const int rc = pp_factor(G, n, n, strideG, D, NB, strideD, batch, info, logdet, false,
+                           static_cast<char*>(ws), resident, stream, pre, nullptr, &L);
   gpfit_prof_end(GP_PROF_POTRF, stream);
   return rc;
 }

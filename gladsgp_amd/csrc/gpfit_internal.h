@@ -36,3 +36,17 @@ long long gpfit_potrf_inv_ws_bytes(int n, int batch);
 int gpfit_gram_lower(const double* X, int n, int d, int ldx, const double* beta, int ldbeta,
                      const double* s, const double* delta, double* G, int ldg,
                      long long strideG, int batch, hipStream_t stream);
+
+// gp_loglik on the persistent factorisation's in-chain mode (chol.hip): G (lower triangle,
+// strideG per problem, ld = n) factorised without L^-1; the chain solves z = L^-1 w by forward
+// substitution over its diagonal inverses D_j (D: NB x NB N doubles per problem, strideD) with
+// the DP tasks' partial sums, and the last workgroup writes ll = -(1/2 |z|^2 + 1/2 logdet)
+// (-inf / NaN + status as nll_reduce) and info_out.  zb holds 2 NB N doubles per problem (zld),
+// zz one double per problem.  Returns 1 (nothing enqueued) when the persistent kernel does not
+// take (n, batch): the caller runs its L^-1 path.  `pre` (the Gram) as gpfit_potrf_inv_event.
+long long gpfit_potrf_loglik_ws_bytes(int n, int batch);
+int gpfit_potrf_loglik(double* G, int n, long long strideG, double* D, long long strideD,
+                       const double* w, int ldw, double* zb, int zld, double* zz, int batch,
+                       int* info, double* logdet, double* ll, int* status, int* info_out,
+                       void* ws, long long ws_bytes, hipStream_t stream,
+                       GpfitPre pre = GpfitPre());

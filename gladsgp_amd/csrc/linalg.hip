@@ -136,8 +136,10 @@ extern "C" int gp_nll(const double* Linv, int ldinv, long long strideInv, int n,
 namespace {
 struct LoglikWs {
   double* G;
-  double* Linv;
+  double* Linv;      // L^-1 path: L^-1; in-chain path: the diagonal inverses D_j
   double* z;
+  double* zb;        // in-chain path: z_j and the DP tasks' partial sums (2 npad per problem)
+  double* zz;        // in-chain path: sum z^2 per problem
   double* logdet;
   int* info;
   int* status;       // sticky internal-error word (gp_loglik_status)
@@ -158,6 +160,10 @@ LoglikWs loglik_carve(void* ws, int n, int batch) {
   off += up(8LL * batch * npad * npad);
   w.z = reinterpret_cast<double*>(p + off);
   off += up(8LL * batch * n);
+  w.zb = reinterpret_cast<double*>(p + off);
+  off += up(8LL * batch * 2 * npad);
+  w.zz = reinterpret_cast<double*>(p + off);
+  off += up(8LL * batch);
   w.logdet = reinterpret_cast<double*>(p + off);
   off += up(8LL * batch);
   w.info = reinterpret_cast<int*>(p + off);
@@ -166,6 +172,8 @@ LoglikWs loglik_carve(void* ws, int n, int batch) {
   off += 256;
   w.pot = p + off;
   w.pot_bytes = gpfit_potrf_inv_ws_bytes(n, batch);
+  if (gpfit_potrf_loglik_ws_bytes(n, batch) > w.pot_bytes)
+    w.pot_bytes = gpfit_potrf_loglik_ws_bytes(n, batch);
   off += up(w.pot_bytes);
   w.bytes = off;
   return w;
@@ -198,8 +206,30 @@ extern "C" int gp_loglik(const double* X, int n, int d, int ldx, const double* b
   if (ws_bytes < c.bytes) return -13;
   if (!ll) return -14;
   const int npad = gp_padded_n(n);
-  int rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, c.G, n, (long long)n * n,
-                            batch, stream);
+  // In-chain path (the persistent factorisation's range): Gram -> factorisation whose chain
+  // also solves z = L^-1 w by forward substitution over its diagonal inverses and writes ll
+  // itself -- no L^-1 tasks, no trmv, no reduction launch (the fit's 24 x 512 gp_loglik: see
+  // DESIGN.md "Metropolis fit").  The Gram is enqueued after the schedule kernel, as in
+  // gp_fit_predict.
+  struct GramArgs {
+    const double *X, *beta, *s, *delta;
+    double* G;
+    int n, d, ldx, ldbeta, batch;
+    hipStream_t st;
+  } ga{X, beta, s, delta, c.G, n, d, ldx, ldbeta, batch, stream};
+  GpfitPre pre;
+  pre.arg = &ga;
+  pre.fn = [](void* a) -> int {
+    const GramArgs& g = *static_cast<const GramArgs*>(a);
+    return gpfit_gram_lower(g.X, g.n, g.d, g.ldx, g.beta, g.ldbeta, g.s, g.delta, g.G, g.n,
+                            (long long)g.n * g.n, g.batch, g.st);
+  };
+  int rc = gpfit_potrf_loglik(c.G, n, (long long)n * n, c.Linv, (long long)npad * npad, w,
+                              batch > 1 ? ldw : n, c.zb, 2 * npad, c.zz, batch, c.info,
+                              c.logdet, ll, c.status, info, c.pot, c.pot_bytes, stream, pre);
+  if (rc <= 0) return rc;
+  rc = gpfit_gram_lower(X, n, d, ldx, beta, ldbeta, s, delta, c.G, n, (long long)n * n,
+                        batch, stream);
   if (rc) return rc;
   rc = gpfit_potrf_inv_event(c.G, n, n, (long long)n * n, c.Linv, npad, (long long)npad * npad,
                              batch, c.info, c.logdet, c.pot, c.pot_bytes, stream, -1, nullptr);

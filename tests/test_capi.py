@@ -281,7 +281,9 @@ def test_persistent_factorisation_leaves_room_for_cross():
     Round 4 found it broken by 10 extra pp_kernel registers (C3 27.7 vs 26.8 ms per step: the
     cross-covariance waited for the whole factorisation) -- this guards the budget."""
     res = _kernel_resources()
-    pp = [v for k, v in res.items() if "pp_kernel" in k]
+    # pp_kernel<false>: the factorisation gp_fit_predict overlaps (pp_kernel<true> is
+    # gp_loglik's in-chain mode, which runs with no cross-covariance beside it)
+    pp = [v for k, v in res.items() if "pp_kernelILb0E" in k]
     cross = [v for k, v in res.items() if "cross_kp_kernelILi8E" in k]
     assert pp and cross, sorted(res)[:20]
     pp, cross = pp[0], cross[0]

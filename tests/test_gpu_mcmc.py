@@ -222,3 +222,40 @@ def test_merged_group_step_equals_two_launches(dev, monkeypatch):
         np.testing.assert_array_equal(recs[1][k], recs[0][k], err_msg=k)
     for k in cnts[0]:
         np.testing.assert_array_equal(cnts[1][k], cnts[0][k], err_msg=str(k))
+
+
+@pytest.mark.parametrize("n,P", [(512, 24), (512, 8), (700, 8), (130, 1), (1000, 3), (64, 2)])
+def test_loglik_in_chain_matches_oracle_and_linv_path(dev, n, P):
+    """gp_loglik on the persistent factorisation's in-chain mode (the chain solves z = L^-1 w by
+    forward substitution over its diagonal inverses, the DP tasks add sum_k L_jk z_k, the last
+    workgroup writes ll; no L^-1 tasks, trmv or reduction) against the oracle, and against the
+    L^-1 path (gp_set_potrf_path(1): blocked sweep + L^-1 + trmv + reduction).  (512, 24) is the
+    fit's speculative group at timing.csv:9; 700 a ragged last tile; 8 and 24 the per-XCD
+    queues."""
+    from gladsgp_amd import _capi
+    d = 8
+    X, w, lam = _problem(n, d, P, seed=n + P)
+    rng = np.random.default_rng(P)
+    betaU = rng.uniform(0.2, 3.0, (d + 1, P))
+    lamUz = rng.uniform(0.5, 3.0, P)
+    lamWs = rng.uniform(200, 3000, P)
+    lamWOs = 120.0
+    ref = mcmc_ref.loglik_pcs(X, w, lam, betaU, lamUz, lamWs, lamWOs)
+    args = (_t(X, dev), _t(betaU[1:].T, dev), _t(1.0 / lamUz, dev),
+            _t(1.0 / lamWs + 1.0 / (lamWOs * lam), dev), _t(w, dev))
+    ws = kernels.LoglikWorkspace(n, P, dev)
+    got = kernels.loglik(*args, ws).cpu().numpy()
+    ws.check_status()
+    assert np.all(ws.info.cpu().numpy() == 0)
+    prev = _capi.lib().gp_set_potrf_path(1)
+    try:
+        ws1 = kernels.LoglikWorkspace(n, P, dev)
+        alt = kernels.loglik(*args, ws1).cpu().numpy()
+    finally:
+        _capi.lib().gp_set_potrf_path(prev)
+    tol = 1e-9 * np.maximum(1.0, np.abs(ref))
+    assert np.all(np.abs(got - ref) <= tol), (got - ref)
+    assert np.all(np.abs(got - alt) <= 1e-11 * np.maximum(1.0, np.abs(alt))), (got - alt)
+    # repeated calls on one workspace: bit-identical (deterministic partial-sum order)
+    again = kernels.loglik(*args, ws).cpu().numpy()
+    assert np.array_equal(again, got)

@@ -10,7 +10,7 @@ cp gladsgp_amd/libgpfit.so gpurun_out/.libgpfit_keep3.so
 for rep in 1 2; do
   for lib in "$@"; do
     cp "$lib" gladsgp_amd/libgpfit.so
-    timeout -k 10 300 python bench.py --workload fit > gpurun_out/${TAG}_one.log 2>&1 || { cat gpurun_out/${TAG}_one.log; cp gpurun_out/.libgpfit_keep3.so gladsgp_amd/libgpfit.so; exit 1; }
+    timeout -k 10 300 python bench.py --workload fit --no-cpu > gpurun_out/${TAG}_one.log 2>&1 || { cat gpurun_out/${TAG}_one.log; cp gpurun_out/.libgpfit_keep3.so gladsgp_amd/libgpfit.so; exit 1; }
     python -c "
 import json
 l=json.loads([x for x in open('gpurun_out/${TAG}_one.log').read().splitlines() if x.startswith('{')][-1])
