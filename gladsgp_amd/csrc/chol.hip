@@ -1702,7 +1702,7 @@ GP_DEV void ll_zstep(const PPArgs& P, int b, int j, int nb, double& zz) {
     for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
     if (r == 0) zz += q;
   }
-  __syncthreads();
+  // (no barrier: z and the partial slots are next read / rewritten behind the step's own)
 }
 
 template <bool LL>
@@ -1768,21 +1768,15 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
         }
     __syncthreads();
     if constexpr (LL) {
-      // y_j = (w_j - zq_j) - L_j,j-1 z_j-1 (L_j,j-1 in g_keep as [col][row] since step j-1)
-      const int r = threadIdx.x & 63, c0 = 16 * (threadIdx.x >> 6);
-      double part = 0.0;
-      if (j >= 1) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c)
-          part = fma(g_keep[(c0 + c) * LP + r], g_ll[kLLZ + c0 + c], part);
-      }
-      g_ll[kLLPart + threadIdx.x] = part;
-      __syncthreads();
+      // y_j = (w_j - zq_j) - L_j,j-1 z_j-1: the last term's four column-quarter partial sums
+      // were formed beside step j-1's SYRK (read after that step's barriers; y is read after
+      // diag_factor_blk's)
       if (threadIdx.x < 64) {
+        const int r = threadIdx.x;
         const double* pq = g_ll + kLLPart + r;
-        g_ll[kLLY + r] = r < nb ? wq - (((pq[0] + pq[64]) + pq[128]) + pq[192]) : 0.0;
+        const double t = j >= 1 ? ((pq[0] + pq[64]) + pq[128]) + pq[192] : 0.0;
+        g_ll[kLLY + r] = r < nb ? wq - t : 0.0;
       }
-      // (read after diag_factor_blk's barriers)
     }
     // (b) factor + invert
     PP_MARK(P, 11, j);
@@ -1828,6 +1822,8 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
     // instead of in front of the flag (n = 4096 1.812 vs 1.824 ms, n = 1024 x 32 0.994 vs
     // 0.998, bit-identical; profiles/r04/ab_zt_ljj.log)
     pp_store_rm(atile(j, j), P.lda, sm.As, nb, true);
+    // (LL) z_j = D_j y_j (D_j in Bs) here, where the chain may wait for SP(j) below anyway
+    if constexpr (LL) ll_zstep(P, b, j, nb, zz);
     __syncthreads();                                    // every wave has read As
     PP_TRACE(P, tb0 + 4, pp_now());
     if (!spref) {
@@ -1846,10 +1842,17 @@ PP_TASK void pp_chain(const PPArgs& P, int b) {
     __syncthreads();
     PP_TRACE(P, tb0 + 6, pp_now());
     pp_store_cm(atile(j + 1, j), P.lda, g_keep, nb1, NB, false);
-    // (LL) z_j = D_j y_j (D_j is still in Bs), stored with L_j+1,j
-    if constexpr (LL) ll_zstep(P, b, j, nb, zz);
     // the next step's SYRK runs while L_j+1,j's stores drain, then its flag goes up
     mma64(g_keep, g_keep, syrk);
+    if constexpr (LL) {
+      // (LL) the quarter sums of L_j+1,j z_j for y_j+1, beside the SYRK (pp_publish's barrier
+      // orders them before the next step reads them)
+      const int r = threadIdx.x & 63, c0 = 16 * (threadIdx.x >> 6);
+      double part = 0.0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) part = fma(g_keep[(c0 + c) * LP + r], g_ll[kLLZ + c0 + c], part);
+      g_ll[kLLPart + threadIdx.x] = part;
+    }
     pp_publish(F + (j + 1) * N + j);
     if constexpr (LL)
       if (threadIdx.x == 0) pp_stflag(F + N * N + j, 1);    // FZ[j]: z_j drained with the above

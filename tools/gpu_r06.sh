@@ -22,7 +22,7 @@ for step in "$@"; do
     field_ab) run field_ab 300 python -u tools/field_ab.py || exit $? ;;
     c4q) run c4q 300 python -u bench.py --workload c4 --no-cpu --steps 5 --warmup 2 || exit $? ;;
     c3q) run c3q 300 python -u bench.py --no-cpu --steps 10 --warmup 3 || exit $? ;;
-    ab_fit) run ab_fit 900 bash tools/ab_fit_libs.sh r06_ab_fit_inner _ab/libgpfit_old.so _ab/libgpfit_new.so || exit $? ;;
+    ab_fit) run ab_fit 900 bash tools/ab_fit_libs.sh r06_ab_fit_inner _ab/libgpfit_old.so _ab/libgpfit_new.so _ab/libgpfit_inchain.so || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
