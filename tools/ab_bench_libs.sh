@@ -12,7 +12,7 @@ for rep in 1 2; do
   for lib in "$@"; do
     cp "$lib" gladsgp_amd/libgpfit.so
     for wl in ${AB_WORKLOADS:-c3 c4}; do
-      st=10; [ $wl = c4 ] && st=5
+      st=10; [ $wl = c4 ] && st=5; [ $wl = c5 ] && st=5
       timeout -k 10 200 python bench.py --workload $wl --steps $st --warmup 2 --no-cpu > gpurun_out/${TAG}_one.log 2>&1 || { cat gpurun_out/${TAG}_one.log; cp gpurun_out/.libgpfit_keep.so gladsgp_amd/libgpfit.so; exit 1; }
       python -c "
 import json

@@ -23,6 +23,8 @@ for step in "$@"; do
     c4q) run c4q 300 python -u bench.py --workload c4 --no-cpu --steps 5 --warmup 2 || exit $? ;;
     c3q) run c3q 300 python -u bench.py --no-cpu --steps 10 --warmup 3 || exit $? ;;
     ab_fit) run ab_fit 900 bash tools/ab_fit_libs.sh r06_ab_fit_inner _ab/libgpfit_old.so _ab/libgpfit_new.so _ab/libgpfit_inchain.so || exit $? ;;
+    ab_trmm) AB_WORKLOADS="c3 c4 c5" run ab_trmm 1000 bash tools/ab_bench_libs.sh r06_ab_trmm_inner _ab/libgpfit_pre_trmm.so _ab/libgpfit_trmm_persist.so || exit $? ;;
+    t_sched) run t_sched 600 $PYT tests/test_gpu_sched.py tests/test_gpu_c3.py tests/test_gpu_c4.py || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
