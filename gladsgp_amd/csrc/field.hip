@@ -41,7 +41,17 @@ namespace {
 #define FIELD_NT 1
 #endif
 template <int KS> constexpr int field_rows() { return KS <= 8 ? 32 : FIELD_ROWS_BIG; }
-constexpr int kFieldCols = 256;              // output columns per block (64 per wave)
+#ifndef FIELD_WAVES
+#define FIELD_WAVES 4
+#endif
+#ifndef FIELD_JT
+#define FIELD_JT 4
+#endif
+constexpr int kFieldWaves = FIELD_WAVES;     // waves per block
+constexpr int kFieldJT = FIELD_JT;           // 16-column MFMA tiles per wave
+constexpr int kFieldThreads = 64 * kFieldWaves;
+constexpr int kFieldWaveCols = 16 * kFieldJT;
+constexpr int kFieldCols = kFieldWaves * kFieldWaveCols;   // output columns per block
 constexpr int kFieldPitch = 68;              // LDS row pitch of a w tile (doubles)
 constexpr int kFieldMaxP = 64;
 
@@ -50,7 +60,7 @@ constexpr int kFieldMaxP = 64;
 // U = npanels x ntiles (one residency round of B blocks: no tail round), reloading its K panel
 // when its range crosses into the next panel.
 template <int KS, bool F32>
-__global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __restrict__ W,
+__global__ __launch_bounds__(kFieldThreads, FIELD_OCC) void field_kernel(const double* __restrict__ W,
                                                        long long ldw, int rows, int P,
                                                        const double* __restrict__ K,
                                                        long long ldk, int ncols,
@@ -61,7 +71,7 @@ __global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __r
                                                        long long ntiles) {
   constexpr int KP = 4 * KS;                              // padded inner dimension
   constexpr int kFieldRows = field_rows<KS>(), RS = kFieldRows / 16;
-  constexpr int NLD = (kFieldRows * KP + 255) / 256;      // w-tile elements per thread
+  constexpr int NLD = (kFieldRows * KP + kFieldThreads - 1) / kFieldThreads;   // per thread
   __shared__ double ws[2][kFieldRows * kFieldPitch];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
@@ -71,14 +81,14 @@ __global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __r
   const long long u1 = units * (blockIdx.x + 1) / gridDim.x;
   if (u0 >= u1) return;                                  // block-uniform
 
-  double b[KS][4];
+  double b[KS][kFieldJT];
   long long cur = -1;                                    // the panel held in b
   auto load_panel = [&](long long panel) {
-    const int c0 = (int)panel * kFieldCols + wv * 64;   // this wave's first column
+    const int c0 = (int)panel * kFieldCols + wv * kFieldWaveCols;   // this wave's first column
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int jt = 0; jt < 4; ++jt) {
+      for (int jt = 0; jt < kFieldJT; ++jt) {
         const int k = 4 * ks + lk, c = c0 + 16 * jt + li;
         b[ks][jt] = (k < P && c < ncols) ? K[(long long)k * ldk + c] : 0.0;
       }
@@ -91,7 +101,7 @@ __global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __r
     const long long r0 = t * kFieldRows;
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
-      const int e = threadIdx.x + 256 * q;
+      const int e = threadIdx.x + kFieldThreads * q;
       const int r = e / KP, k = e % KP;
       pre[q] = (e < kFieldRows * KP && k < P && r0 + r < rows) ? W[(r0 + r) * ldw + k] : 0.0;
     }
@@ -99,7 +109,7 @@ __global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __r
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
-      const int e = threadIdx.x + 256 * q;
+      const int e = threadIdx.x + kFieldThreads * q;
       if (e < kFieldRows * KP) ws[buf][(e / KP) * kFieldPitch + e % KP] = pre[q];
     }
   };
@@ -114,11 +124,11 @@ __global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __r
     const bool more = u + 1 < u1;
     const long long tn = t + 1 == ntiles ? 0 : t + 1;
     if (more) load_tile(tn);                             // in flight under the MFMAs
-    f64x4 acc[RS][4];
+    f64x4 acc[RS][kFieldJT];
 #pragma unroll
     for (int rs = 0; rs < RS; ++rs)
 #pragma unroll
-      for (int jt = 0; jt < 4; ++jt) acc[rs][jt] = zero4();
+      for (int jt = 0; jt < kFieldJT; ++jt) acc[rs][jt] = zero4();
     const double* wt = ws[buf];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -126,17 +136,18 @@ __global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __r
       for (int rs = 0; rs < RS; ++rs) {
         const double a = wt[(16 * rs + li) * kFieldPitch + 4 * ks + lk];
 #pragma unroll
-        for (int jt = 0; jt < 4; ++jt) acc[rs][jt] = mfma16x16x4(a, b[ks][jt], acc[rs][jt]);
+        for (int jt = 0; jt < kFieldJT; ++jt)
+          acc[rs][jt] = mfma16x16x4(a, b[ks][jt], acc[rs][jt]);
       }
     }
     // epilogue: row 16 rs + lk + 4 q, column 16 jt + li of the tile
     const long long r0 = t * kFieldRows;
-    const int c0 = (int)panel * kFieldCols + wv * 64;
+    const int c0 = (int)panel * kFieldCols + wv * kFieldWaveCols;
     // the back-transform's sd / mu of the wave's 4 columns: read per tile (L1 hits), not
     // held across the K loop (the K panel and accumulators take 192 of the 256 registers)
-    double s_c[4], m_c[4];
+    double s_c[kFieldJT], m_c[kFieldJT];
 #pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
+    for (int jt = 0; jt < kFieldJT; ++jt) {
       const int c = c0 + 16 * jt + li;
       const bool ok = sd != nullptr && c < ncols;
       s_c[jt] = ok ? sd[c] : 1.0;
@@ -150,7 +161,7 @@ __global__ __launch_bounds__(256, FIELD_OCC) void field_kernel(const double* __r
         if (r >= rows) continue;
         const double e = err ? err[r] : 0.0;
 #pragma unroll
-        for (int jt = 0; jt < 4; ++jt) {
+        for (int jt = 0; jt < kFieldJT; ++jt) {
           const int c = c0 + 16 * jt + li;
           if (c >= ncols) continue;
           double v = acc[rs][jt][q];
@@ -196,9 +207,11 @@ hipError_t launch_field(const double* W, long long ldw, int rows, int P, const d
   const long long npanels = gp_ceil_div(ncols, kFieldCols);
   constexpr int kFieldRows = field_rows<KS>();
   const long long ntiles = ((long long)rows + kFieldRows - 1) / kFieldRows;
-  long long blocks = (long long)FIELD_OCC * field_num_cus();   // one residency round
+  // one residency round: FIELD_OCC waves per SIMD (launch_bounds' second argument), 4 SIMDs
+  long long blocks = (long long)field_num_cus() *
+                     (FIELD_OCC * 4 >= kFieldWaves ? FIELD_OCC * 4 / kFieldWaves : 1);
   if (blocks > npanels * ntiles) blocks = npanels * ntiles;
-  hipLaunchKernelGGL((field_kernel<KS, F32>), dim3((unsigned)blocks), dim3(256), 0, stream, W,
+  hipLaunchKernelGGL((field_kernel<KS, F32>), dim3((unsigned)blocks), dim3(kFieldThreads), 0, stream, W,
                      ldw, rows, P, K, ldk, ncols, sd, mu, err, Y, ldy, ntiles);
   return hipGetLastError();
 }

@@ -13,7 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # 32-row tiles at one block per CU 4.52-4.75, one block per CU 5.27
 VARIANTS = {
     "base": [],
-    "plain": ["-DFIELD_NT=0"],
+    "w4j2o3": ["-DFIELD_JT=2", "-DFIELD_OCC=3"],
+    "w8j4": ["-DFIELD_WAVES=8"],
+    "w8j2r32": ["-DFIELD_WAVES=8", "-DFIELD_JT=2", "-DFIELD_ROWS_BIG=32"],
+    "w4j2o3r32": ["-DFIELD_JT=2", "-DFIELD_OCC=3", "-DFIELD_ROWS_BIG=32"],
 }
 
 
