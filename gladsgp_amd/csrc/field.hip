@@ -33,7 +33,7 @@ namespace {
 #define FIELD_ROWS_BIG 16
 #endif
 #ifndef FIELD_OCC
-#define FIELD_OCC 2
+#define FIELD_OCC 3
 #endif
 // non-temporal output stores (the field is written once and not re-read by this kernel):
 // 3.26 vs 3.78 ms at C5 (profiles/r06/r06c_field_ab.log), same bits
@@ -45,7 +45,7 @@ template <int KS> constexpr int field_rows() { return KS <= 8 ? 32 : FIELD_ROWS_
 #define FIELD_WAVES 4
 #endif
 #ifndef FIELD_JT
-#define FIELD_JT 4
+#define FIELD_JT 2
 #endif
 constexpr int kFieldWaves = FIELD_WAVES;     // waves per block
 constexpr int kFieldJT = FIELD_JT;           // 16-column MFMA tiles per wave

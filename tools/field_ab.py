@@ -10,13 +10,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # round 6 first pass (profiles/r06/r06c_field_ab.log): base (plain stores) 3.78 ms, nt 3.26,
-# 32-row tiles at one block per CU 4.52-4.75, one block per CU 5.27
+# 32-row tiles at one block per CU 4.52-4.75, one block per CU 5.27. Second pass
+# (r06i_field_ab.log): JT 4 / 2 blocks per CU 3.13, JT 2 / 3 per CU 3.02 (adopted), 8-wave
+# blocks 3.18-3.26, 32-row tiles at JT 2 3.13.
 VARIANTS = {
     "base": [],
-    "w4j2o3": ["-DFIELD_JT=2", "-DFIELD_OCC=3"],
-    "w8j4": ["-DFIELD_WAVES=8"],
-    "w8j2r32": ["-DFIELD_WAVES=8", "-DFIELD_JT=2", "-DFIELD_ROWS_BIG=32"],
-    "w4j2o3r32": ["-DFIELD_JT=2", "-DFIELD_OCC=3", "-DFIELD_ROWS_BIG=32"],
+    "w4j4o2": ["-DFIELD_JT=4", "-DFIELD_OCC=2"],
+    "w4j1o4": ["-DFIELD_JT=1", "-DFIELD_OCC=4"],
+    "w4j1o4r32": ["-DFIELD_JT=1", "-DFIELD_OCC=4", "-DFIELD_ROWS_BIG=32"],
 }
 
 
