@@ -419,6 +419,331 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Column-resident prediction with the cross-covariance fused in, for npad <= 512 (C5's
+// 512-point design, the fit's PC GPs).  At small n the pair kernel's 128 x 128 tiles spend 16
+// of a block's 8 (NI + 1) K steps in diagonal blocks (16 of 40 at n = 512) whose stage loads
+// and barriers cost a step each for 56% of a step's MFMAs, and its K* operand makes a round
+// trip through HBM (the cross-covariance chunk written, then read by every row-tile pair).
+// Here a panel is 32 test points of one problem, and one block computes ALL npad rows of
+// V = L^-1 K*^T for it:
+//   * K*'s npad x 32 panel lives in LDS (128 KB at npad = 512) and is produced in place, 32
+//     rows (a chunk) at a time, by the block's own threads: s exp(-sum (sqrt(beta)(x_k -
+//     x*_j))^2) with cross_kp_kernel's exact arithmetic (the same Kt values bit for bit), one
+//     exp per element -- no cross-covariance kernel, no Kt slab in HBM;
+//   * L^-1 (1 MB lower triangle per problem at n = 512, L2-resident: panels are problem-major,
+//     so the chip works through one problem's panels at a time) streams straight into
+//     registers as MFMA A fragments by buffer loads (wave-uniform offset + four per-lane
+//     offsets: no vector address arithmetic), one 16-k step ahead;
+//   * 8 waves, wave w owning the 16-row tiles {w, 15 - w, 16 + w, 31 - w} (the first RT of
+//     them: equal sums of (T + 1), i.e. equal MFMA work), both 16-column MFMA tiles;
+//   * tile T meets L^-1 at k-steps j <= T; activity is resolved per chunk (steps 2c, 2c + 1:
+//     tile i takes part when T_i >= 2c, its step 2c + 1 then reading, when T_i = 2c, the zero
+//     16 x 16 block above the diagonal -- zeroed by gp_potrf_inv / gp_trtri; the packed layout
+//     does not store it, so those loads select 0).  T ascends with i, so the active tiles are
+//     a suffix i >= F and the chunks split into segments of constant F, each its own
+//     straight-line loop (no per-step branches, no accumulator copies);
+//   * persistent: a block walks panels p = blockIdx.x, + gridDim.x, ... as one stream of
+//     chunks, so everything the next panel needs before its first MFMA -- its first chunk of
+//     K*, its first A fragments, its test points, sqrt(beta), z -- is produced or loaded under
+//     the current panel's last chunks (which hold few MFMAs) instead of in a prologue;
+//   * one barrier per chunk, one more per panel for the epilogue, which reduces sum V z and
+//     sum V^2 over the panel's rows and writes mean / var directly (no slab, no finalize).
+// Every global load is issued unconditionally (at a clamped in-bounds address when its value
+// is not needed): the same number of loads on every path keeps the compiler's vmcnt waits
+// counted, so prefetches stay in flight across the MFMAs.
+// SLAB: K* read from a materialised cross-covariance chunk instead (gp_predict_solve after
+// gp_predict_cross, and d > 8), two chunks ahead through registers -- the same Kt values, so
+// every entry point gives the same bits at npad <= 512.
+// Sums run k ascending in every tile (the pair kernel runs some tiles diagonal-block first), so
+// results equal the pair path to rounding, not bit for bit; they do not depend on the chunking.
+#ifndef RES_COLS
+#define RES_COLS 64
+#endif
+#ifndef RES_OCC
+#define RES_OCC 2                              // waves per SIMD (launch bound)
+#endif
+constexpr int kResCols = RES_COLS;             // test points per panel
+// RES_WIDE: 4 RT waves of two row tiles each (16 waves at npad = 512: 4 per SIMD); else 8
+// waves of RT tiles
+#ifndef RES_WIDE
+#define RES_WIDE 0
+#endif
+// timing probes only (wrong results): 1 = no MFMAs, 2 = A fragments loaded once
+#ifndef RES_PROBE
+#define RES_PROBE 0
+#endif
+__host__ __device__ constexpr int res_waves(int RT) { return RES_WIDE ? 4 * RT : 8; }
+constexpr int kResMaxWaves = 16;
+constexpr int kResMaxPad = 512;
+constexpr int kResD = 8;                       // design dimensions (d <= 8)
+
+struct ResArgs {
+  const double* Linv;      // padded (column k at k * ld) or tile-packed (linv_col, PACKED)
+  long long sL;
+  int ld;
+  int n, d, mv, npanel;    // test points of this launch, ceil(mv / kResCols)
+  int batch;
+  const double* X;
+  int ldx;
+  const double* Xs;        // the launch's first test point
+  int ldxs;
+  const double* beta;
+  int ldbeta;
+  const double* s;
+  const double* s_pred;
+  const double* z;
+  long long zld;
+  double* mean;            // the launch's first test point's column
+  double* var;
+  int ldo;
+  const double* kt;        // SLAB: the chunk's cross-covariance (row k of problem b at
+  long long sK;            //   kt + b * sK + k * mc)
+  int mc;
+};
+
+template <bool PACKED, int RT, bool SLAB>
+__global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void trmm_res_kernel(
+    const ResArgs a) {
+  constexpr int NW = res_waves(RT);            // waves
+  constexpr int kResThreads = 64 * NW;
+  constexpr int TW = RT * 8 / NW;              // 16-row tiles per wave
+  constexpr int NPAD = 128 * RT;
+  constexpr int NCH = NPAD / 32;               // 32-row K* chunks per panel (even)
+  constexpr int NJ = NPAD / 16;                // 16-k steps per panel
+  constexpr int RING = 32 * kResD;             // one chunk's design rows
+  constexpr int BCH = 32 * kResCols;           // one chunk of K*
+  constexpr int NCT = kResCols / 16;           // 16-column MFMA tiles per panel
+  constexpr int NPR = kResThreads / kResCols;  // K* rows one production pass covers
+  constexpr int NH = (32 + NPR - 1) / NPR;     // production passes per chunk
+  constexpr bool RAG = 32 % NPR != 0;          // (the last pass covers part of the chunk)
+  __shared__ __attribute__((aligned(16))) double Bs[2 * BCH];   // K* chunks c, c + 1
+  __shared__ double tab[64];
+  __shared__ double xring[4 * RING];           // design rows: 3 ring slots + a scratch slot
+  __shared__ double xsc[kResD * kResCols];     // sqrt(beta)-scaled test points, [dim][point]
+  __shared__ double red[NW * 2 * kResCols];
+  __shared__ double zs[NPAD];
+  const int g = blockIdx.x;
+  const int b = g / a.npanel, P = g - b * a.npanel;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lk = lane >> 4;
+  const int pc = tid & (kResCols - 1), rp = tid / kResCols;   // K* production: column, row
+  const int xrow = tid >> 3, xd = tid & (kResD - 1);          // ring fill: design row, dim
+  int T[TW];                                   // snake: equal sums of (T + 1) per wave
+#pragma unroll
+  for (int i = 0; i < TW; ++i) T[i] = (i & 1) ? NW * i + NW - 1 - w : NW * i + w;
+  int voff[4];                                 // lane (li, lk): row li, column 4 q + lk
+#pragma unroll
+  for (int q = 0; q < 4; ++q) voff[q] = ((4 * q + lk) * a.ld + li) * 8;
+  // raw inputs are loaded at clamped in-bounds indices and masked where they are stored
+  const double bq = (!SLAB && xd < a.d)        // sqrt(beta[b][xd]), 0 past d
+                        ? __builtin_sqrt(a.beta[(long long)b * a.ldbeta + xd]) : 0.0;
+  auto xval = [&](int c) {                     // design row 32 c + xrow, dimension xd
+    const int k = 32 * c + xrow;
+    return a.X[(long long)(k < a.n ? k : a.n - 1) * a.ldx + (xd < a.d ? xd : 0)];
+  };
+  auto xscale = [&](int c, double v) {         // cross_kp's xk
+    return (32 * c + xrow < a.n && xd < a.d) ? v * bq : 0.0;
+  };
+  const double* ktc = a.kt + b * a.sK + P * kResCols + pc;    // SLAB: column pc's chunk
+  auto kval = [&](int c, int h) {
+    const int r = rp + NPR * h;
+    return ktc[(long long)(32 * c + (RAG && r >= 32 ? 31 : r)) * a.mc];
+  };
+  // K* chunk c in slot c & 1; row r's 64 doubles with the 16-column halves of each 32-column
+  // group swapped in odd rows: the 16-lane groups of a B fragment read (rows k .. k+3) then
+  // cover all 64 banks twice, conflict-free
+  auto bslot = [&](int c, int h) {
+    const int r = rp + NPR * h;
+    return Bs + (c & 1) * BCH + r * kResCols + (pc ^ (16 * (r & 1)));
+  };
+  const double sb = SLAB ? 0.0 : a.s[b];
+  const bool col_ok = P * kResCols + pc < a.mv;
+  // element h of chunk c of K*, from design-row slot `slot`
+  auto produce_one = [&](int c, int slot, int h) {
+    const int r = rp + NPR * h, k = 32 * c + r;
+    if (RAG && r >= 32) return;
+    const double* xc = xsc + pc;               // [dim][point]: consecutive lanes, banks
+    const double* xk = xring + slot * RING + r * kResD;
+    double e = 0.0;
+#pragma unroll
+    for (int dd = 0; dd < kResD; ++dd) {
+      const double t = xk[dd] - xc[dd * kResCols];
+      e = fma(t, t, e);
+    }
+    const double v = sb * exp_neg_tab(e, tab);
+    *bslot(c, h) = (col_ok && k < a.n) ? v : 0.0;
+  };
+  auto produce = [&](int c, int slot) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h) produce_one(c, slot, h);
+  };
+
+  // ---- L^-1 fragments (buffer loads: wave-uniform offset + per-lane voff)
+  const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(a.Linv + b * a.sL), 0, 0x7fffffff, 0x00020000);
+  auto frag = [&](int i, int je, int q) -> double {
+    if (PACKED) {
+      const int k = 16 * je + 4 * q + lk;
+      return (T[i] >= je) ? a.Linv[b * a.sL + linv_col(k, NPAD) + 16 * T[i] + li] : 0.0;
+    }
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(lrs, voff[q],
+                                                        (16 * je * a.ld + 16 * T[i]) * 8, 0);
+    return __longlong_as_double(((long long)v[1] << 32) | v[0]);
+  };
+  double av[TW][4];
+  f64x4 acc[TW][NCT];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[i][ct] = zero4();
+  const int sw = 16 * (lk & 1);
+  // step j's MFMAs for tiles F .. RT-1; each fragment, once used, is reloaded with step
+  // j + 1's (one register set: the reload of substep q runs under substeps q + 1 .. 3 and the
+  // next step's first substeps)
+  auto mstep = [&](auto F, int j) {
+    if constexpr (decltype(F)::value < TW) {
+      const int jn = (j + 1 < NJ) ? j + 1 : NJ - 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double* br = Bs + ((j >> 1) & 1) * BCH + ((j & 1) * 16 + 4 * q + lk) * kResCols;
+        double bv[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) bv[ct] = br[(16 * ct + li) ^ sw];
+        static_for<decltype(F)::value, TW, 1>([&](auto I) {
+#if RES_PROBE != 1
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[I][ct] = mfma16x16x4(av[I][q], bv[ct], acc[I][ct]);
+#else
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[I][ct][0] += av[I][q] * bv[ct];
+#endif
+#if RES_PROBE != 2
+          av[I][q] = frag(I, jn, q);
+#endif
+        });
+      }
+    }
+  };
+
+  // ---- prologue: test points, z, design rows of chunks 0 and 1, K* chunk 0, A(0)
+  {
+    const double zv = a.z[b * a.zld + (tid < NPAD ? tid : 0)];
+    if (SLAB) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+        if (!RAG || rp + NPR * h < 32) *bslot(0, h) = kval(0, h);
+    } else {
+      if (tid < 64) tab[tid] = kExp2Tab[tid];
+      double xs[kResCols / 32];                // test points xrow + 32 h, dimension xd
+#pragma unroll
+      for (int h = 0; h < kResCols / 32; ++h) {
+        const int c_ = P * kResCols + xrow + 32 * h;
+        xs[h] = a.Xs[(long long)(c_ < a.mv ? c_ : a.mv - 1) * a.ldxs + (xd < a.d ? xd : 0)];
+      }
+      const double x0 = xval(0), x1 = xval(1);
+      if (tid < RING) {
+#pragma unroll
+        for (int h = 0; h < kResCols / 32; ++h)
+          xsc[xd * kResCols + 32 * h + xrow] =
+              (P * kResCols + xrow + 32 * h < a.mv && xd < a.d) ? xs[h] * bq : 0.0;
+        xring[tid] = xscale(0, x0);
+        xring[RING + tid] = xscale(1, x1);
+      }
+    }
+    if (tid < NPAD) zs[tid] = zv;
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) av[i][q] = frag(i, 0, q);
+    __syncthreads();
+    if (!SLAB) produce(0, 0);
+    __syncthreads();
+  }
+
+  // ---- chunks: K* chunk c + 1 (produced now; SLAB: loaded now, stored after the MFMAs) into
+  // the slot chunk c - 1 used, design rows of chunk c + 2 into ring slot s2, MFMAs of steps
+  // 2c and 2c + 1.  Tile i takes part in chunk c when T_i >= 2c (its step 2c + 1 then reads,
+  // when T_i = 2c, the zero 16 x 16 block above the diagonal -- zeroed by gp_potrf_inv /
+  // gp_trtri; the packed layout does not store it, so those loads select 0).  T ascends with
+  // i, so the active tiles are a suffix i >= F: the chunks split into segments of constant F,
+  // each its own straight-line loop.
+  int s1 = 1, s2 = 2;                          // design-row slots of chunks c + 1, c + 2
+  auto chunk = [&](auto F, int c) {
+    const int cf = (c + 2 < NCH) ? c + 2 : NCH - 1;   // (past the end: a harmless refill)
+    double xn = 0.0, kn[NH];
+    if (SLAB) {
+      const int cn = (c + 1 < NCH) ? c + 1 : NCH - 1;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) kn[h] = kval(cn, h);
+    } else {
+      xn = xval(cf);
+    }
+    if (!SLAB && c + 1 < NCH) produce(c + 1, s1);
+    // (spreading this production between the MFMA substeps measured 1.6% slower)
+    mstep(F, 2 * c);
+    mstep(F, 2 * c + 1);
+    if (SLAB) {
+      if (c + 1 < NCH) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+          if (!RAG || rp + NPR * h < 32) *bslot(c + 1, h) = kn[h];
+      }
+    } else {
+      xring[(tid < RING ? s2 : 3) * RING + (tid & (RING - 1))] = xscale(cf, xn);
+    }
+    __syncthreads();
+    s1 = s2;
+    s2 = (s2 == 2) ? 0 : s2 + 1;
+  };
+  int c = 0;
+  static_for<0, TW + 1, 1>([&](auto F) {
+    constexpr int f = decltype(F)::value;
+    int cend = (f < TW) ? T[f < TW ? f : 0] / 2 + 1 : NCH;   // chunks with T_f >= 2c
+    if (cend > NCH) cend = NCH;
+#pragma unroll 1
+    for (; c < cend; ++c) chunk(F, c);
+  });
+
+  // ---- epilogue: per column sum V z and sum V^2 over the wave's rows (C layout: lane l, reg
+  // r holds row 16 T + (l >> 4) + 4 r, column l & 15), then over the 8 waves in a fixed order
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    double sm = 0.0, sv = 0.0;
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double v = acc[i][ct][r];
+        sm = fma(v, zs[16 * T[i] + lk + 4 * r], sm);
+        sv = fma(v, v, sv);
+      }
+    sm += __shfl_xor(sm, 16, 64);
+    sv += __shfl_xor(sv, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    sv += __shfl_xor(sv, 32, 64);
+    if (lk == 0) {
+      red[(w * 2 + 0) * kResCols + ct * 16 + li] = sm;
+      red[(w * 2 + 1) * kResCols + ct * 16 + li] = sv;
+    }
+  }
+  __syncthreads();
+  if (tid < kResCols) {
+    double sm = 0.0, sv = 0.0;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      sm += red[(v * 2 + 0) * kResCols + tid];
+      sv += red[(v * 2 + 1) * kResCols + tid];
+    }
+    const int cg = P * kResCols + tid;
+    if (cg < a.mv) {
+      a.mean[(long long)b * a.ldo + cg] = sm;
+      a.var[(long long)b * a.ldo + cg] = a.s_pred[b] - sv;
+    }
+  }
+}
+
 // mean / var of test points [j0, j0 + mv): column j's partial sums sit in the slab of chunk
 // j / mc, counted from j0's chunk (slabs pslab doubles apart after `part`; pslab = 0 when every
 // chunk reuses one slab).
@@ -799,6 +1124,119 @@ hipError_t trmm_launch(const Plan& p, int ch0, int ch1, const double* kt, long l
   return hipGetLastError();
 }
 
+// The column-resident kernel (trmm_res_kernel) serves every npad <= 512 prediction, with the
+// cross-covariance fused in when d <= 8 (res_fused) and from a materialised chunk otherwise;
+// GPFIT_TRMM_RES=0 in the environment forces the cross-covariance + pair-TRMM path (A/B runs).
+bool res_eligible(int npad) {
+  static const int env = [] {
+    const char* e = std::getenv("GPFIT_TRMM_RES");
+    return e ? std::atoi(e) : 1;
+  }();
+  return env != 0 && npad <= kResMaxPad;
+}
+// (GPFIT_TRMM_RES=2: the materialised-chunk kernel for every d, an A/B of the fusion)
+bool res_fused(int d) {
+  static const int env = [] {
+    const char* e = std::getenv("GPFIT_TRMM_RES");
+    return e ? std::atoi(e) : 1;
+  }();
+  return env != 2 && d <= kResD;
+}
+
+// mean / var of test points [j0, j0 + mv) of every problem in one launch (problem-major blocks).
+hipError_t res_launch(int npad, const LinvRef& L, int n, int d, const double* X, int ldx,
+                      const double* Xs, int ldxs, int j0, int mv, const double* beta,
+                      int ldbeta, const double* s, const double* s_pred, const double* z,
+                      long long zld, double* mean, double* var, int ldo, int batch,
+                      const double* kt, long long sK, int mc, hipStream_t st) {
+  ResArgs a;
+  a.Linv = L.p;
+  a.sL = L.stride;
+  a.ld = L.ld;
+  a.n = n;
+  a.d = d;
+  a.mv = mv;
+  a.npanel = gp_ceil_div(mv, kResCols);
+  a.batch = batch;
+  a.X = X;
+  a.ldx = ldx;
+  a.Xs = Xs + (long long)j0 * ldxs;
+  a.ldxs = ldxs;
+  a.beta = beta;
+  a.ldbeta = ldbeta;
+  a.s = s;
+  a.s_pred = s_pred;
+  a.z = z;
+  a.zld = zld;
+  a.mean = mean + j0;
+  a.var = var + j0;
+  a.ldo = ldo;
+  a.kt = kt;
+  a.sK = sK;
+  a.mc = mc;
+  const long long total = (long long)batch * a.npanel;
+#define GP_RES_K(PK, RT, SL)                                                               \
+  hipLaunchKernelGGL((trmm_res_kernel<PK, RT, SL>), dim3((unsigned)total),                  \
+                     dim3(64 * res_waves(RT)), \
+                     0, st, a)
+#define GP_RES(RT)                                                            \
+  do {                                                                        \
+    if (kt) {                                                                 \
+      if (L.packed) GP_RES_K(true, RT, true); else GP_RES_K(false, RT, true); \
+    } else {                                                                  \
+      if (L.packed) GP_RES_K(true, RT, false); else GP_RES_K(false, RT, false); \
+    }                                                                         \
+  } while (0)
+  switch (npad / 128) {
+    case 1: GP_RES(1); break;
+    case 2: GP_RES(2); break;
+    case 3: GP_RES(3); break;
+    case 4: GP_RES(4); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef GP_RES
+#undef GP_RES_K
+  return hipGetLastError();
+}
+
+// trmm_res_kernel over all m test points, one launch per plan chunk (another stream's kernels
+// can interleave between launches, as with the TRMM chunks).  K* source: fused (d <= 8), the
+// prepared slabs of gp_predict_cross, or each chunk's cross-covariance built into slab 0 just
+// before its launch.
+enum class ResSrc { Fused, Prepared, Serial };
+
+hipError_t res_all(const Plan& p, const WS& w, ResSrc src, const LinvRef& L, int n, int m, int d,
+                   const double* X, int ldx, const double* Xs, int ldxs, const double* beta,
+                   int ldbeta, const double* s, const double* s_pred, const double* z,
+                   long long zld, double* mean, double* var, int ldo, int batch,
+                   hipStream_t st) {
+  const bool one = src != ResSrc::Serial;    // one timing pair around all launches
+  if (one) gpfit_prof_begin_n(GP_PROF_TRMM, st, p.nchunks);
+  for (int ch = 0; ch < p.nchunks; ++ch) {
+    const int j0 = ch * p.mc;
+    const int mv = (m - j0 < p.mc) ? (m - j0) : p.mc;
+    const double* kt = nullptr;
+    hipError_t e;
+    if (src == ResSrc::Prepared) {
+      kt = w.kt + (long long)ch * p.slab_elems;
+    } else if (src == ResSrc::Serial) {
+      gpfit_prof_begin(GP_PROF_CROSS, st);
+      if ((e = cross_chunk(p, ch, w.kt, X, ldx, Xs, ldxs, n, m, d, beta, ldbeta, s, batch,
+                           st)) != hipSuccess)
+        return e;
+      gpfit_prof_end(GP_PROF_CROSS, st);
+      kt = w.kt;
+    }
+    if (!one) gpfit_prof_begin(GP_PROF_TRMM, st);
+    e = res_launch(p.npad, L, n, d, X, ldx, Xs, ldxs, j0, mv, beta, ldbeta, s, s_pred, z, zld,
+                   mean, var, ldo, batch, kt, (long long)p.mc * p.npad, p.mc, st);
+    if (e != hipSuccess) return e;
+    if (!one) gpfit_prof_end(GP_PROF_TRMM, st);
+  }
+  if (one) gpfit_prof_end(GP_PROF_TRMM, st);
+  return hipSuccess;
+}
+
 // Every chunk's TRMM into its own slab, then one finalize over all m points.  With `ready`
 // (gp_fit_predict on a context), chunk ch's TRMM first waits for ready[ch], the event after
 // that chunk's cross-covariance on the aux stream.
@@ -877,6 +1315,11 @@ extern "C" int gp_predict_ex(const double* Linv, int ldinv, long long strideInv,
   hipError_t e;
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   if (!z) GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, stream));
+  if (res_eligible(p.npad)) {
+    GP_CK(res_all(p, w, res_fused(d) ? ResSrc::Fused : ResSrc::Serial, L, n, m, d, X, ldx, Xs,
+                  ldxs, beta, ldbeta, s, s_pred, zz, zld, mean, var, ldo, batch, stream));
+    return 0;
+  }
   // chunk by chunk: cross-covariance, TRMM, mean / var, reusing one slab -- except that a
   // merged last chunk (trmm_merge_last) has its own second slab, and its TRMM and finalize
   // cover the chunk before it too
@@ -1043,6 +1486,11 @@ extern "C" int gp_predict_solve(const double* Linv, int ldinv, long long strideI
 #define GP_CK(x) do { e = (x); if (e != hipSuccess) return GPFIT_ERR_HIP - (int)e; } while (0)
   const LinvRef L{Linv, ldinv, strideInv, false};
   GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, stream));
+  if (res_eligible(p.npad)) {
+    GP_CK(res_all(p, w, ResSrc::Prepared, L, n, m, 0, nullptr, 0, nullptr, 0, nullptr, 0,
+                  nullptr, s_pred, w.z, p.npad, mean, var, ldo, batch, stream));
+    return 0;
+  }
   GP_CK(solve_all(p, w, L, w.z, p.npad, m, s_pred, mean, var, ldo, batch, stream, nullptr,
                   p.nchunks, [](int) { return hipSuccess; }));
 #undef GP_CK
@@ -1237,6 +1685,15 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
                              w.pot, p.bytes - p.off_pot, fact, k_late > 0 ? k_late : -1,
                              (S && k_late > 0) ? S->e_late : nullptr, pre);
   if (rc) return rc;
+  const LinvRef L{Linv, ldinv, strideInv, false};
+  if (res_eligible(p.npad)) {
+    // the cross-covariance is produced inside the prediction kernel (d <= 8; otherwise chunk
+    // by chunk before each launch on pred): nothing forks onto aux
+    GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, pred));
+    GP_CK(res_all(p, w, res_fused(d) ? ResSrc::Fused : ResSrc::Serial, L, n, m, d, X, ldx, Xs,
+                  ldxs, beta, ldbeta, s, s_pred, w.z, p.npad, mean, var, ldo, batch, pred));
+    return 0;
+  }
   if (S) GP_CK(hipStreamWaitEvent(aux, S->e_late, 0));
   // chunks whose cross-covariance runs on aux, beside the factorisation and the earlier TRMMs
   // (all by default; the rest run on pred just before their TRMM: gp_ctx_set_aux_chunks)
@@ -1256,7 +1713,6 @@ extern "C" int gp_fit_predict(const double* X, int ldx, const double* Xs, int ld
   // the dispatcher interleaves another stream's kernels between launches, so a concurrent
   // factorisation is not starved behind a 25 ms grid (measured: 14 ms vs 3 ms per potrf).
   if (S && n_aux > 0) GP_CK(hipEventRecord(S->e_chunk[n_aux - 1], aux));   // after the end event
-  const LinvRef L{Linv, ldinv, strideInv, false};
   GP_CK(trmv_pred(p.npad, w.zp, L, w_hat, ldw, n, batch, w.z, p.npad, pred));
   GP_CK(solve_all(p, w, L, w.z, p.npad, m, s_pred, mean, var, ldo, batch, pred,
                   S ? S->e_chunk.data() : nullptr, n_aux, [&](int ch) {

@@ -13,7 +13,7 @@ cp "$SRC" gladsgp_amd/csrc/.variant.hip
   -c gladsgp_amd/csrc/.variant.hip -o "$OBJ" 2>&1 | grep -v ds128 || true
 rm -f gladsgp_amd/csrc/.variant.hip
 objs=""
-for f in gram chol predict linalg profile blas eig comm rng mcmc host_rng; do
+for f in gram chol predict linalg profile blas eig comm rng mcmc host_rng field; do
   [ "$f" = "$REP" ] || objs="$objs gladsgp_amd/_obj/$f.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" "$OBJ" $objs -ldl

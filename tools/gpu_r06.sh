@@ -24,6 +24,12 @@ for step in "$@"; do
     c3q) run c3q 300 python -u bench.py --no-cpu --steps 10 --warmup 3 || exit $? ;;
     ab_fit) run ab_fit 900 bash tools/ab_fit_libs.sh r06_ab_fit_inner _ab/libgpfit_old.so _ab/libgpfit_new.so _ab/libgpfit_inchain.so || exit $? ;;
     ab_trmm) AB_WORKLOADS="c3 c4 c5" run ab_trmm 1000 bash tools/ab_bench_libs.sh r06_ab_trmm_inner _ab/libgpfit_pre_trmm.so _ab/libgpfit_trmm_persist.so || exit $? ;;
+    ab_diag) AB_WORKLOADS="c4 c5" run ab_diag 900 bash tools/ab_bench_libs.sh r06_ab_diag_inner _ab/libgpfit_base.so _ab/libgpfit_diag1.so _ab/libgpfit_diag2.so || exit $? ;;
+    pmc_c5) run pmc_c5_traffic 700 bash tools/pmc_traffic.sh c5 && run pmc_c5_mfma 400 bash tools/pmc_mfma.sh c5 || exit $? ;;
+    ab_zpre) AB_WORKLOADS="c3 c4 c5" run ab_zpre 1000 bash tools/ab_bench_libs.sh r06_ab_zpre_inner _ab/libgpfit_base.so _ab/libgpfit_zpre.so || exit $? ;;
+    ab_res) run ab_res 900 bash tools/ab_res.sh r06_ab_res_inner || exit $? ;;
+    pmc_res) run pmc_res 600 bash tools/pmc_res.sh r06_pmc_res || exit $? ;;
+    ab_res2) run ab_res2 1100 bash tools/ab_res2.sh r06_ab_res2_inner "${AB_LIBS:-_ab/libgpfit_narrow.so}" "${AB_MODES:-2 1}" || exit $? ;;
     t_sched) run t_sched 600 $PYT tests/test_gpu_sched.py tests/test_gpu_c3.py tests/test_gpu_c4.py || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -1,6 +1,6 @@
 #!/bin/bash
 # HBM traffic per kernel from PMC counters (separate passes: FETCH_SIZE, WRITE_SIZE).
-#   tools/pmc_traffic.sh [c3|c4]   -> gpurun_out/pmc_traffic.json | pmc_traffic_c4.json
+#   tools/pmc_traffic.sh [c3|c4|c5]   -> gpurun_out/pmc_traffic.json | pmc_traffic_c4.json
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 WL=${1:-c3}
@@ -31,8 +31,10 @@ if t:
     if WL == "c3":
         # 6 launches per step since round 5 (the 1696-point tail runs merged with chunk 6)
         n, m, chunk, batch, launches = 4096, 100000, 16384, 1, 6
-    else:                                # C4: 32 GPs, n = 1024, 8192-point chunks
+    elif WL == "c4":                     # C4: 32 GPs, n = 1024, 8192-point chunks
         n, m, chunk, batch, launches = 1024, 100000, 8192, 32, 13
+    else:                                # C5: 64 PC GPs, n = 512, 13 TRMM launches per step
+        n, m, chunk, batch, launches = 512, 100000, 7936, 64, 13
     L = 8.0 * n * (n + 1) / 2 * batch    # L^-1 lower triangles
     kt = 8.0 * n * m / launches * batch  # mean Kt chunk per launch
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of "
