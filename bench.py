@@ -1109,11 +1109,13 @@ REF_FIT_MCMC_S = 1405.595
 
 
 def fit_roofline(model, mcmc_s: float, sweeps: int, reps: int = 20) -> dict:
-    """The fit's dominant kernel: the batched persistent factorisation (pp_kernel, Cholesky +
-    L^-1) inside every gp_loglik of a sweep.  One gp_loglik per speculative group at that
-    group's batch ((2^g - 1) P problems at n = 512), at the fitted model's parameter values,
-    timed ``reps`` times with the library's event pair around the factorisation (GP_PROF_POTRF)
-    and with torch events around whole calls; flop = batch (n^3/3 + n^3/3)."""
+    """The fit's dominant kernel: the batched persistent factorisation inside every gp_loglik of
+    a sweep, in its log-likelihood mode (pp_kernel<true>: Cholesky with the forward solve
+    z = L^-1 w and the reduction to ll in the same launch, no L^-1).  One gp_loglik per
+    speculative group at that group's batch ((2^g - 1) P problems at n = 512), at the fitted
+    model's parameter values, timed ``reps`` times with the library's event pair around the
+    factorisation (GP_PROF_POTRF) and with torch events around whole calls;
+    flop = batch (n^3/3 + n^2)."""
     from gladsgp_amd import kernels
     sm = model._sampler()
     n, d, P, dev = sm.n, sm.d, sm.P, sm.dev
@@ -1153,10 +1155,11 @@ def fit_roofline(model, mcmc_s: float, sweeps: int, reps: int = 20) -> dict:
     sweep_ms = 1e3 * mcmc_s / sweeps
     fact_per_sweep = sum(per_call[B]["factorisation_ms"] for B in sizes)
     Bmax = max(sizes)
-    fl = Bmax * 2.0 * n ** 3 / 3.0
+    fl = Bmax * (n ** 3 / 3.0 + float(n) ** 2)
     ach = fl / (per_call[Bmax]["factorisation_ms"] * 1e-3) / 1e12
-    return {"kernel": f"pp_kernel (batched Cholesky + L^-1 in gp_loglik, {Bmax} problems at "
-                      f"n = {n})", "bound": "mfma", "achieved": round(ach, 3),
+    return {"kernel": f"pp_kernel<true> (gp_loglik's batched Cholesky + in-chain forward "
+                      f"solve, {Bmax} problems at n = {n})", "bound": "mfma",
+            "achieved": round(ach, 3),
             "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
             "avg_launch_ms": round(per_call[Bmax]["factorisation_ms"], 4),
@@ -1166,7 +1169,8 @@ def fit_roofline(model, mcmc_s: float, sweeps: int, reps: int = 20) -> dict:
                             for B, c in per_call.items()},
             "factorisation_share_of_sweep": round(fact_per_sweep / sweep_ms, 4),
             "sweep_ms": round(sweep_ms, 4),
-            "work_note": "batch x (n^3/3 potrf + n^3/3 triangular inverse) per factorisation; "
+            "work_note": "batch x (n^3/3 potrf + n^2 forward solve) per call; the chain of "
+                         "n/64 dependent diagonal steps bounds it, not the flops (DESIGN §4.3); "
                          "timed outside the sampler's HIP graphs at the fitted parameters"}
 
 

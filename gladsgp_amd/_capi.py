@@ -129,6 +129,7 @@ SIGNATURES = {
     "gp_profile_read": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
     "gp_set_poll_budget": (c_ll, [c_ll]),
     "gp_set_potrf_path": (c_int, [c_int]),
+    "gp_set_predict_path": (c_int, [c_int]),
 }
 
 PROF_GRAM, PROF_POTRF, PROF_TRMM, PROF_CROSS = 0, 1, 2, 3
@@ -182,6 +183,11 @@ def lib() -> ctypes.CDLL:
             continue
         fn.restype = res
         fn.argtypes = args
+    # GPFIT_TRMM_RES (A/B runs, bench.py / tools/ab_res*.sh): 0 = cross-covariance chunks + the
+    # pair TRMM everywhere, 2 = the column-resident kernel from materialised chunks
+    mode = os.environ.get("GPFIT_TRMM_RES", "1")
+    if mode in ("0", "2") and getattr(handle, "gp_set_predict_path", None) is not None:
+        handle.gp_set_predict_path(1 if mode == "0" else 2)
     _LIB = handle
     return handle
 

@@ -1125,23 +1125,14 @@ hipError_t trmm_launch(const Plan& p, int ch0, int ch1, const double* kt, long l
 }
 
 // The column-resident kernel (trmm_res_kernel) serves every npad <= 512 prediction, with the
-// cross-covariance fused in when d <= 8 (res_fused) and from a materialised chunk otherwise;
-// GPFIT_TRMM_RES=0 in the environment forces the cross-covariance + pair-TRMM path (A/B runs).
+// cross-covariance fused in when d <= 8 (res_fused) and from a materialised chunk otherwise.
+// gp_set_predict_path (A/B hook): 1 forces the cross-covariance + pair-TRMM path, 2 the
+// column-resident kernel from materialised chunks for every d.
+std::atomic<int> g_predict_path{0};
 bool res_eligible(int npad) {
-  static const int env = [] {
-    const char* e = std::getenv("GPFIT_TRMM_RES");
-    return e ? std::atoi(e) : 1;
-  }();
-  return env != 0 && npad <= kResMaxPad;
+  return g_predict_path.load(std::memory_order_relaxed) != 1 && npad <= kResMaxPad;
 }
-// (GPFIT_TRMM_RES=2: the materialised-chunk kernel for every d, an A/B of the fusion)
-bool res_fused(int d) {
-  static const int env = [] {
-    const char* e = std::getenv("GPFIT_TRMM_RES");
-    return e ? std::atoi(e) : 1;
-  }();
-  return env != 2 && d <= kResD;
-}
+bool res_fused(int d) { return g_predict_path.load(std::memory_order_relaxed) != 2 && d <= kResD; }
 
 // mean / var of test points [j0, j0 + mv) of every problem in one launch (problem-major blocks).
 hipError_t res_launch(int npad, const LinvRef& L, int n, int d, const double* X, int ldx,
@@ -1442,6 +1433,14 @@ extern "C" int gp_unpack_linv(const double* P, int n, double* Linv, int ldinv,
                      (long long)ldinv, const_cast<double*>(P), 1);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : GPFIT_ERR_HIP - (int)e;
+}
+
+// Prediction path for later enqueues (process-wide A/B hook): 0 = automatic (trmm_res_kernel at
+// npad <= 512, cross-covariance fused when d <= 8; else cross-covariance chunks + the pair TRMM),
+// 1 = always chunks + pair TRMM, 2 = trmm_res_kernel from materialised chunks at npad <= 512.
+// Returns the previous value.
+extern "C" int gp_set_predict_path(int path) {
+  return g_predict_path.exchange((path == 1 || path == 2) ? path : 0);
 }
 
 extern "C" int gp_predict_cross(const double* X, int ldx, const double* Xs, int ldxs, int n,

@@ -520,6 +520,15 @@ long long gp_set_poll_budget(long long polls);
  * kernel with one shared task queue for every batch.  Returns the previous setting. */
 int gp_set_potrf_path(int path);
 
+/* A-B hook, process-wide: the prediction path of gp_predict / gp_predict_ex / gp_fit_predict /
+ * gp_predict_solve enqueued afterwards.  0 = automatic (at gp_padded_n(n) <= 512 the
+ * column-resident kernel, the cross-covariance produced inside it when d <= 8 and read from
+ * materialised chunks otherwise; above, cross-covariance chunks + the row-pair TRMM), 1 = always
+ * cross-covariance chunks + the row-pair TRMM, 2 = the column-resident kernel from materialised
+ * chunks at every d.  Paths 0 and 2 give the same bits; path 1 agrees to rounding.  Returns the
+ * previous setting.  (Python: GPFIT_TRMM_RES=0 / 2 in the environment sets 1 / 2 at load.) */
+int gp_set_predict_path(int path);
+
 #ifdef __cplusplus
 }
 #endif

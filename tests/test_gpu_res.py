@@ -118,3 +118,26 @@ def test_res_nonfinite_hyperparameters_propagate(dev):
     mu, var = kernels.predict(ch, Xd, Xsd, bad, sd, sd, Wd)
     assert torch.equal(mu[0], good_m[0]) and torch.equal(var[0], good_v[0])
     assert torch.isnan(mu[1]).all() and torch.isnan(var[1]).all()
+
+
+def test_predict_path_hook(dev):
+    """gp_set_predict_path: 2 (the column-resident kernel from materialised chunks) gives the
+    fused path's bits; 1 (cross-covariance chunks + the pair TRMM) agrees to rounding."""
+    from gladsgp_amd import _capi, kernels
+    n, m, B, d = 300, 3000, 2, 8
+    X, Xs, betas, W, s, delta = _problem(n, m, B, d, 17)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+    Xd, Xsd, bd, Wd, sd, dd = t(X), t(Xs), t(betas), t(W), t(s), t(delta)
+    lib = _capi.lib()
+    prev = lib.gp_set_predict_path(0)
+    try:
+        ref = kernels.fit_predict(Xd, Xsd, bd, sd, dd, sd, Wd)[:2]
+        lib.gp_set_predict_path(2)
+        slab = kernels.fit_predict(Xd, Xsd, bd, sd, dd, sd, Wd)[:2]
+        lib.gp_set_predict_path(1)
+        pair = kernels.fit_predict(Xd, Xsd, bd, sd, dd, sd, Wd)[:2]
+    finally:
+        assert lib.gp_set_predict_path(prev) in (0, 1, 2)
+    assert torch.equal(slab[0], ref[0]) and torch.equal(slab[1], ref[1])
+    assert float((pair[0] - ref[0]).abs().max()) <= 1e-10 * max(1.0, float(ref[0].abs().max()))
+    assert float((pair[1] - ref[1]).abs().max()) <= 1e-12 * float(sd.max())
