@@ -35,7 +35,11 @@ struct LMat {
 
 // The cyclic Jacobi sweep loop and the descending sort, on views A and V (the same operations
 // in the same order whichever memory holds them: bit-identical results).
-template <typename MA, typename MV>
+// FUSE (the LDS form): a round's row and column rotations in one phase, one thread per 2 x 2
+// block (row pair t, column pair u) applying J_t^T then J_u to its four elements -- every
+// element sees the two-phase form's operations in the same order, so the bits are the same --
+// with V's column rotations beside them: two barriers per round instead of three.
+template <bool FUSE, typename MA, typename MV>
 GP_DEV int syevj_solve(MA A, MV V, int r, int max_sweeps, double tol, double* cs, double* sn,
                        int* pp, int* qq, double* red, int* done) {
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -104,6 +108,47 @@ GP_DEV int syevj_solve(MA A, MV V, int r, int max_sweeps, double tol, double* cs
         qq[tid] = q;
       }
       __syncthreads();
+      if (FUSE) {
+        for (int g = tid; g < npair * npair; g += nt) {
+          const int t = g % npair, u = g / npair;
+          const int p = pp[t], q = qq[t], pu = pp[u], qu = qq[u];
+          const bool rq = q < r, cq = qu < r;
+          // the block after J_t^T (rows p, q), column pu (suffix 0) and qu (suffix 1)
+          double xp0 = A(p, pu), xp1 = cq ? A(p, qu) : 0.0;
+          double xq0 = 0.0, xq1 = 0.0;
+          if (rq) {
+            const double c = cs[t], s = sn[t];
+            const double y0 = A(q, pu), y1 = cq ? A(q, qu) : 0.0;
+            xq0 = s * xp0 + c * y0;
+            xp0 = c * xp0 - s * y0;
+            xq1 = s * xp1 + c * y1;
+            xp1 = c * xp1 - s * y1;
+          }
+          if (cq) {
+            const double c = cs[u], s = sn[u];
+            A(p, pu) = c * xp0 - s * xp1;
+            A(p, qu) = s * xp0 + c * xp1;
+            if (rq) {
+              A(q, pu) = c * xq0 - s * xq1;
+              A(q, qu) = s * xq0 + c * xq1;
+            }
+          } else {
+            A(p, pu) = xp0;
+            if (rq) A(q, pu) = xq0;
+          }
+        }
+        for (int g = tid; g < npair * r; g += nt) {
+          const int k = g / npair, t = g % npair;
+          const int p = pp[t], q = qq[t];
+          if (q >= r) continue;
+          const double c = cs[t], s = sn[t];
+          const double x = V(k, p), y = V(k, q);
+          V(k, p) = c * x - s * y;
+          V(k, q) = s * x + c * y;
+        }
+        __syncthreads();
+        continue;
+      }
       // phase 1: rows p, q of A   (A <- J^T A)
       for (int g = tid; g < npair * r; g += nt) {
         const int k = g / npair, t = g % npair;
@@ -183,7 +228,7 @@ __global__ __launch_bounds__(1024) void syevj_kernel(double* __restrict__ A, int
   __shared__ double ws[kMaxR];
   __shared__ int done;
   const GMat Ag{A, lda}, Vg{V, ldv};
-  const int sweep = syevj_solve(Ag, Vg, r, max_sweeps, tol, cs, sn, pp, qq, red, &done);
+  const int sweep = syevj_solve<false>(Ag, Vg, r, max_sweeps, tol, cs, sn, pp, qq, red, &done);
   syevj_finish(Ag, Vg, r, sweep, W, Vg, perm, ws, sweeps_out, want_sqrt);
 }
 
@@ -209,7 +254,7 @@ __global__ __launch_bounds__(1024) void syevj_lds_kernel(double* __restrict__ A,
     Al(i, j) = A[i + (long long)j * lda];
   }
   __syncthreads();
-  const int sweep = syevj_solve(Al, Vl, r, max_sweeps, tol, cs, sn, pp, qq, red, &done);
+  const int sweep = syevj_solve<true>(Al, Vl, r, max_sweeps, tol, cs, sn, pp, qq, red, &done);
   syevj_finish(Al, Vl, r, sweep, W, GMat{V, ldv}, perm, ws, sweeps_out, want_sqrt);
   for (int g = tid; g < r * r; g += nt) {
     const int i = g % r, j = g / r;

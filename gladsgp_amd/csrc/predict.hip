@@ -681,7 +681,6 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
       xn = xval(cf);
     }
     if (!SLAB && c + 1 < NCH) produce(c + 1, s1);
-    // (spreading this production between the MFMA substeps measured 1.6% slower)
     mstep(F, 2 * c);
     mstep(F, 2 * c + 1);
     if (SLAB) {

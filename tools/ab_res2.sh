@@ -15,7 +15,7 @@ for rep in 1 2; do
 import json
 l=json.loads([x for x in open('gpurun_out/${TAG}_one.log').read().splitlines() if x.startswith('{')][-1])
 r=l['roofline']; ph=l['phases_ms']
-print('%-22s RES=$res c5 step %.3f ms  %.2fM pred/s  predict %.3f ms  trmm %.4f ms/launch x %d (%.1f TF/s)' % ('$(basename $lib)', l['ms_per_step'], l['value']/1e6, ph['predict'], r['avg_launch_ms'], r['launches'], r['achieved']))
+print('%-22s RES=$res c5 step %.3f ms  %.2fM pred/s  svd %.3f  predict %.3f  get_y %.3f ms  trmm %.4f ms/launch x %d (%.1f TF/s)' % ('$(basename $lib)', l['ms_per_step'], l['value']/1e6, ph['svd'], ph['predict'], ph['get_y'], r['avg_launch_ms'], r['launches'], r['achieved']))
 " >> gpurun_out/$TAG.log || exit 1
     done
   done
