@@ -469,7 +469,8 @@ constexpr int kResCols = RES_COLS;             // test points per panel
 #ifndef RES_WIDE
 #define RES_WIDE 0
 #endif
-// timing probes only (wrong results): 1 = no MFMAs, 2 = A fragments loaded once
+// timing probes only (wrong results): 1 = no MFMAs, 2 = A fragments loaded once, 3 = no
+// per-chunk barrier
 #ifndef RES_PROBE
 #define RES_PROBE 0
 #endif
@@ -517,9 +518,9 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
   constexpr int NPR = kResThreads / kResCols;  // K* rows one production pass covers
   constexpr int NH = (32 + NPR - 1) / NPR;     // production passes per chunk
   constexpr bool RAG = 32 % NPR != 0;          // (the last pass covers part of the chunk)
-  __shared__ __attribute__((aligned(16))) double Bs[2 * BCH];   // K* chunks c, c + 1
+  __shared__ __attribute__((aligned(16))) double Bs[4 * BCH];   // K* chunks c .. c + 3
   __shared__ double tab[64];
-  __shared__ double xring[4 * RING];           // design rows: 3 ring slots + a scratch slot
+  __shared__ double xring[9 * RING];           // design rows: chunk k in slot k & 7; scratch
   __shared__ double xsc[kResD * kResCols];     // sqrt(beta)-scaled test points, [dim][point]
   __shared__ double red[NW * 2 * kResCols];
   __shared__ double zs[NPAD];
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
   // cover all 64 banks twice, conflict-free
   auto bslot = [&](int c, int h) {
     const int r = rp + NPR * h;
-    return Bs + (c & 1) * BCH + r * kResCols + (pc ^ (16 * (r & 1)));
+    return Bs + (c & 3) * BCH + r * kResCols + (pc ^ (16 * (r & 1)));
   };
   const double sb = SLAB ? 0.0 : a.s[b];
   const bool col_ok = P * kResCols + pc < a.mv;
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
       const int jn = (j + 1 < NJ) ? j + 1 : NJ - 1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const double* br = Bs + ((j >> 1) & 1) * BCH + ((j & 1) * 16 + 4 * q + lk) * kResCols;
+        const double* br = Bs + ((j >> 1) & 3) * BCH + ((j & 1) * 16 + 4 * q + lk) * kResCols;
         double bv[NCT];
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) bv[ct] = br[(16 * ct + li) ^ sw];
@@ -627,13 +628,15 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
     }
   };
 
-  // ---- prologue: test points, z, design rows of chunks 0 and 1, K* chunk 0, A(0)
+  // ---- prologue: test points, z, design rows of chunks 0 .. 3, K* chunks 0 and 1, A(0)
   {
     const double zv = a.z[b * a.zld + (tid < NPAD ? tid : 0)];
     if (SLAB) {
 #pragma unroll
-      for (int h = 0; h < NH; ++h)
-        if (!RAG || rp + NPR * h < 32) *bslot(0, h) = kval(0, h);
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+          if (!RAG || rp + NPR * h < 32) *bslot(c, h) = kval(c, h);
     } else {
       if (tid < 64) tab[tid] = kExp2Tab[tid];
       double xs[kResCols / 32];                // test points xrow + 32 h, dimension xd
@@ -642,14 +645,16 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
         const int c_ = P * kResCols + xrow + 32 * h;
         xs[h] = a.Xs[(long long)(c_ < a.mv ? c_ : a.mv - 1) * a.ldxs + (xd < a.d ? xd : 0)];
       }
-      const double x0 = xval(0), x1 = xval(1);
+      double x4[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x4[c] = xval(c < NCH ? c : NCH - 1);
       if (tid < RING) {
 #pragma unroll
         for (int h = 0; h < kResCols / 32; ++h)
           xsc[xd * kResCols + 32 * h + xrow] =
               (P * kResCols + xrow + 32 * h < a.mv && xd < a.d) ? xs[h] * bq : 0.0;
-        xring[tid] = xscale(0, x0);
-        xring[RING + tid] = xscale(1, x1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xring[c * RING + tid] = xscale(c, x4[c]);
       }
     }
     if (tid < NPAD) zs[tid] = zv;
@@ -658,43 +663,49 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
 #pragma unroll
       for (int q = 0; q < 4; ++q) av[i][q] = frag(i, 0, q);
     __syncthreads();
-    if (!SLAB) produce(0, 0);
+    if (!SLAB) {
+      produce(0, 0);
+      produce(1, 1);
+    }
     __syncthreads();
   }
 
-  // ---- chunks: K* chunk c + 1 (produced now; SLAB: loaded now, stored after the MFMAs) into
-  // the slot chunk c - 1 used, design rows of chunk c + 2 into ring slot s2, MFMAs of steps
-  // 2c and 2c + 1.  Tile i takes part in chunk c when T_i >= 2c (its step 2c + 1 then reads,
+  // ---- chunks: K* chunk c + 2 (produced now; SLAB: loaded now, stored after the MFMAs) into
+  // the slot chunk c - 2 used, design rows of chunk c + 4 into slot (c + 4) & 7, MFMAs of
+  // steps 2c and 2c + 1, and a barrier after every odd chunk only: whatever chunk c writes is
+  // read from chunk c + 2 on, and what it overwrites was last read at chunk c - 2, so one
+  // barrier always lies between (a barrier per chunk cost 6.5%: r06af, no-barrier probe).
+  // Tile i takes part in chunk c when T_i >= 2c (its step 2c + 1 then reads,
   // when T_i = 2c, the zero 16 x 16 block above the diagonal -- zeroed by gp_potrf_inv /
   // gp_trtri; the packed layout does not store it, so those loads select 0).  T ascends with
   // i, so the active tiles are a suffix i >= F: the chunks split into segments of constant F,
   // each its own straight-line loop.
-  int s1 = 1, s2 = 2;                          // design-row slots of chunks c + 1, c + 2
   auto chunk = [&](auto F, int c) {
-    const int cf = (c + 2 < NCH) ? c + 2 : NCH - 1;   // (past the end: a harmless refill)
+    // (past the end: a harmless refill of the last chunk's slot with its own values)
+    const int cf = (c + 4 < NCH) ? c + 4 : NCH - 1;
     double xn = 0.0, kn[NH];
     if (SLAB) {
-      const int cn = (c + 1 < NCH) ? c + 1 : NCH - 1;
+      const int cn = (c + 2 < NCH) ? c + 2 : NCH - 1;
 #pragma unroll
       for (int h = 0; h < NH; ++h) kn[h] = kval(cn, h);
     } else {
       xn = xval(cf);
     }
-    if (!SLAB && c + 1 < NCH) produce(c + 1, s1);
+    if (!SLAB && c + 2 < NCH) produce(c + 2, (c + 2) & 7);
     mstep(F, 2 * c);
     mstep(F, 2 * c + 1);
     if (SLAB) {
-      if (c + 1 < NCH) {
+      if (c + 2 < NCH) {
 #pragma unroll
         for (int h = 0; h < NH; ++h)
-          if (!RAG || rp + NPR * h < 32) *bslot(c + 1, h) = kn[h];
+          if (!RAG || rp + NPR * h < 32) *bslot(c + 2, h) = kn[h];
       }
     } else {
-      xring[(tid < RING ? s2 : 3) * RING + (tid & (RING - 1))] = xscale(cf, xn);
+      xring[(tid < RING ? (cf & 7) : 8) * RING + (tid & (RING - 1))] = xscale(cf, xn);
     }
-    __syncthreads();
-    s1 = s2;
-    s2 = (s2 == 2) ? 0 : s2 + 1;
+#if RES_PROBE != 3
+    if (c & 1) __syncthreads();
+#endif
   };
   int c = 0;
   static_for<0, TW + 1, 1>([&](auto F) {
