@@ -87,10 +87,12 @@ def test_res_matches_oracle_and_is_bitwise_across_paths(dev, n, m, B, d):
     assert np.array_equal(var.cpu().numpy(), ref_v[:, :pre])
 
 
-@pytest.mark.parametrize("n,B", [(200, 1), (512, 2)])
-def test_res_packed_linv_bitwise(dev, n, B):
+@pytest.mark.parametrize("n,B,d", [(200, 1, 8), (512, 2, 8), (300, 2, 12)])
+def test_res_packed_linv_bitwise(dev, n, B, d):
+    """The tile-packed L^-1 gives the padded layout's bits, fused (d <= 8) and from
+    materialised chunks (d > 8)."""
     from gladsgp_amd import kernels
-    X, Xs, betas, W, s, delta = _problem(n, 4000, B, 8, 5 * n + B)
+    X, Xs, betas, W, s, delta = _problem(n, 4000, B, d, 5 * n + B)
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
     Xd, Xsd, bd, Wd, sd, dd = t(X), t(Xs), t(betas), t(W), t(s), t(delta)
     ch = kernels.cholesky_inverse(kernels.gram(Xd, bd, sd, dd, batch=B))
@@ -141,3 +143,15 @@ def test_predict_path_hook(dev):
     assert torch.equal(slab[0], ref[0]) and torch.equal(slab[1], ref[1])
     assert float((pair[0] - ref[0]).abs().max()) <= 1e-10 * max(1.0, float(ref[0].abs().max()))
     assert float((pair[1] - ref[1]).abs().max()) <= 1e-12 * float(sd.max())
+
+
+def test_res_boundary_513_uses_pair_path_and_matches_oracle(dev):
+    """npad 512 -> 640 at n = 513: the row-pair path; both sides of the boundary agree with the
+    oracle at the prediction tolerance."""
+    from gladsgp_amd import kernels
+    for n in (512, 513):
+        X, Xs, betas, W, s, delta = _problem(n, 2500, 2, 8, n)
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+        mean, var, _ = kernels.fit_predict(t(X), t(Xs), t(betas), t(s), t(delta), t(s), t(W))
+        idx = np.arange(0, 2500, 7)
+        _oracle_check(X, Xs, W, betas, s, delta, mean.cpu().numpy(), var.cpu().numpy(), idx)
