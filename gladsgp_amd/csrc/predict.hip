@@ -34,6 +34,12 @@ constexpr int BK = 16;    // K step
 constexpr long long kDefaultChunkElems = 256ll << 20;  // <= 2 GB of Kt per chunk
 constexpr int kDefaultChunk = 8192;                   // test points per chunk (batches)
 constexpr int kDefaultChunkSingle = 16384;            // ... and for one GP
+// Non-temporal cross-covariance stores (the chunk, 2.15 GB at C4, is read back by the TRMM from
+// HBM either way): C4 59.1-59.6 -> 58.7-58.8 ms per step, C3 unchanged
+// (profiles/r06/r06ai_ab_cross_nt.log)
+#ifndef CROSS_NT
+#define CROSS_NT 1
+#endif
 
 // Cross-covariance chunk, k-major as the TRMM streams it:
 //   Kt[k * mc + c] = s * exp(-sum beta (X[k] - Xs[c])^2)
@@ -83,8 +89,13 @@ __global__ __launch_bounds__(256) void cross_kp_kernel(
     // exp unconditionally, then select: padding rows / columns have finite (zeroed) inputs,
     // and a conditional exp costs an exec-mask branch around each call
     const double v0 = sb * exp_neg_tab(e0, tab), v1 = sb * exp_neg_tab(e1, tab);
+#if CROSS_NT
+    __builtin_nontemporal_store((col_ok && k < n) ? v0 : 0.0, o + (long long)k * mc + c);
+    __builtin_nontemporal_store((col_ok && k + 1 < n) ? v1 : 0.0, o + (long long)(k + 1) * mc + c);
+#else
     o[(long long)k * mc + c] = (col_ok && k < n) ? v0 : 0.0;
     o[(long long)(k + 1) * mc + c] = (col_ok && k + 1 < n) ? v1 : 0.0;
+#endif
   }
 }
 

@@ -32,6 +32,7 @@ for step in "$@"; do
     ab_res2) run ab_res2 1100 bash tools/ab_res2.sh r06_ab_res2_inner "${AB_LIBS:-_ab/libgpfit_narrow.so}" "${AB_MODES:-2 1}" || exit $? ;;
     prof_c3) run prof_c3 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r06_${tag}_prof_c3 -o c3 -- python -u bench.py --no-cpu --steps 10 --warmup 3 || exit $? ;;
     lat) run lat 300 python -u bench.py --workload latency || exit $? ;;
+    ab_cross) AB_WORKLOADS="c3 c4" run ab_cross 1000 bash tools/ab_bench_libs.sh r06_ab_cross_inner _ab/libgpfit_crossbase.so _ab/libgpfit_crossnt.so || exit $? ;;
     t_sched) run t_sched 600 $PYT tests/test_gpu_sched.py tests/test_gpu_c3.py tests/test_gpu_c4.py || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
