@@ -436,10 +436,10 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
 // of a block's 8 (NI + 1) K steps in diagonal blocks (16 of 40 at n = 512) whose stage loads
 // and barriers cost a step each for 56% of a step's MFMAs, and its K* operand makes a round
 // trip through HBM (the cross-covariance chunk written, then read by every row-tile pair).
-// Here a panel is 32 test points of one problem, and one block computes ALL npad rows of
-// V = L^-1 K*^T for it:
-//   * K*'s npad x 32 panel lives in LDS (128 KB at npad = 512) and is produced in place, 32
-//     rows (a chunk) at a time, by the block's own threads: s exp(-sum (sqrt(beta)(x_k -
+// Here a panel is kResCols = 64 test points of one problem, and one block computes ALL npad
+// rows of V = L^-1 K*^T for it:
+//   * K*'s panel passes through a four-chunk LDS ring (64 KB), produced 32 rows (a chunk) at
+//     a time, two chunks ahead, by the block's own threads: s exp(-sum (sqrt(beta)(x_k -
 //     x*_j))^2) with cross_kp_kernel's exact arithmetic (the same Kt values bit for bit), one
 //     exp per element -- no cross-covariance kernel, no Kt slab in HBM;
 //   * L^-1 (1 MB lower triangle per problem at n = 512, L2-resident: panels are problem-major,
@@ -454,12 +454,11 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
 //     does not store it, so those loads select 0).  T ascends with i, so the active tiles are
 //     a suffix i >= F and the chunks split into segments of constant F, each its own
 //     straight-line loop (no per-step branches, no accumulator copies);
-//   * persistent: a block walks panels p = blockIdx.x, + gridDim.x, ... as one stream of
-//     chunks, so everything the next panel needs before its first MFMA -- its first chunk of
-//     K*, its first A fragments, its test points, sqrt(beta), z -- is produced or loaded under
-//     the current panel's last chunks (which hold few MFMAs) instead of in a prologue;
-//   * one barrier per chunk, one more per panel for the epilogue, which reduces sum V z and
-//     sum V^2 over the panel's rows and writes mean / var directly (no slab, no finalize).
+//   * one block per panel (a persistent form that streamed a block's panels as one chunk
+//     sequence, loading the next panel's inputs under the last chunks, measured no faster:
+//     profiles/r06/r06ah_ab_res_persistent.log);
+//   * one barrier per two chunks, one more per panel for the epilogue, which reduces sum V z
+//     and sum V^2 over the panel's rows and writes mean / var directly (no slab, no finalize).
 // Every global load is issued unconditionally (at a clamped in-bounds address when its value
 // is not needed): the same number of loads on every path keeps the compiler's vmcnt waits
 // counted, so prefetches stay in flight across the MFMAs.
@@ -481,7 +480,7 @@ constexpr int kResCols = RES_COLS;             // test points per panel
 #define RES_WIDE 0
 #endif
 // timing probes only (wrong results): 1 = no MFMAs, 2 = A fragments loaded once, 3 = no
-// per-chunk barrier
+// chunk barriers, 5 = no K* production in the chunks, 6 = neither production nor barriers
 #ifndef RES_PROBE
 #define RES_PROBE 0
 #endif
@@ -702,7 +701,9 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
     } else {
       xn = xval(cf);
     }
+#if RES_PROBE != 5 && RES_PROBE != 6
     if (!SLAB && c + 2 < NCH) produce(c + 2, (c + 2) & 7);
+#endif
     mstep(F, 2 * c);
     mstep(F, 2 * c + 1);
     if (SLAB) {
@@ -714,7 +715,7 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
     } else {
       xring[(tid < RING ? (cf & 7) : 8) * RING + (tid & (RING - 1))] = xscale(cf, xn);
     }
-#if RES_PROBE != 3
+#if RES_PROBE != 3 && RES_PROBE != 6
     if (c & 1) __syncthreads();
 #endif
   };

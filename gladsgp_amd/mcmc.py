@@ -181,6 +181,19 @@ def uniforms_per_sweep(d: int, P: int) -> int:
     return 2 * ((d + 1) * P + 2 * P + 1)
 
 
+def default_spec(n: int, P: int, updates: int) -> int:
+    """Speculative group size with the least modelled sweep time: ceil(updates / s) batched
+    gp_loglik calls of (2^s - 1) P problems each, a call costing the longer of the
+    factorisation's chain (~25 us per 64-column step) and its work (~4.8 us per n = 512 problem,
+    scaled by n^3).  Fitted on MI355X (profiles/r06/r06al_ab_spec.log: 24 problems 0.21 ms, 56
+    0.26, 120 0.58 at n = 512); it picks spec 3 at the fit's n = 512, P = 8.  Speed only: every
+    spec gives the same chain."""
+    def sweep(s):
+        call = max(0.025 * -(-n // 64), 0.0048 * (2 ** s - 1) * P * (n / 512.0) ** 3)
+        return -(-updates // s) * call
+    return min(range(1, _capi.MCMC_MAX_GROUP + 1), key=sweep)
+
+
 class GPUSampler:
     """Component-wise Metropolis over the P PC-GPs of one emulator, all state on the device.
 
@@ -192,12 +205,14 @@ class GPUSampler:
     (profiles/r03/ab_mcmc_graph.log; round 2 measured the opposite while the factorisation
     still allocated its scratch inside every call).  Both paths run the same in-place sweep.
 
-    ``spec`` (default 2; GPFIT_MCMC_SPEC): likelihood-changing updates per batched gp_loglik,
-    evaluated speculatively for every outcome of the group's earlier updates (see _sweep).  At
-    n = 512 a factorisation is latency-bound (its 64-column chain), so evaluating 3P problems
-    costs about what P did: spec 2 takes a sweep from 11 gp_loglik calls to 6, 3.79 -> 2.86 ms
-    per sweep, the fit 5.05 -> 4.04 s; spec 3 (7P problems, worker-bound) 3.0 ms
-    (profiles/r03/ab_mcmc_spec.log).
+    ``spec`` (default: default_spec(n, P, d + 3); GPFIT_MCMC_SPEC overrides): likelihood-
+    changing updates per batched gp_loglik, evaluated speculatively for every outcome of the
+    group's earlier updates (see _sweep).  At n = 512 a factorisation is latency-bound (its
+    64-column chain), so evaluating 3P problems costs about what P did: spec 2 took a sweep from
+    11 gp_loglik calls to 6, 3.79 -> 2.86 ms per sweep (profiles/r03/ab_mcmc_spec.log).  With
+    the in-chain likelihood (round 6) 7P = 56 problems cost 0.26 ms per call against 0.21 for
+    24, so spec 3 (4 calls) wins at P = 8: 1.278 -> 1.054 ms per sweep, the fit 1.67 -> 1.41-1.44
+    s (profiles/r06/r06al_ab_spec.log).
     """
 
     def __init__(self, X: torch.Tensor, w_hat: torch.Tensor, LamSim: torch.Tensor,
@@ -239,7 +254,8 @@ class GPUSampler:
         self._bgraph = {}
         self.st = None
         if spec is None:
-            spec = int(os.environ.get("GPFIT_MCMC_SPEC", "2"))
+            spec = int(os.environ.get("GPFIT_MCMC_SPEC", "0")) or default_spec(self.n, self.P,
+                                                                               self.d + 3)
         if spec < 1:
             raise ValueError("spec (updates per speculative group) must be >= 1")
         # the likelihood-changing updates of a sweep, in mcmcList order (betaU row 0, the

@@ -92,3 +92,16 @@ def test_spec_must_be_positive(cpu_loglik):
     with pytest.raises(ValueError):
         mcmc.GPUSampler(X, torch.zeros((2, 4), dtype=F64), torch.ones(2, dtype=F64),
                         mcmc.ModelParams(2, 2), spec=0)
+
+
+def test_default_spec_cost_model():
+    """default_spec: spec 3 at the fit's n = 512, P = 8 (11 updates; r06al measured 1.054 vs
+    1.278 ms per sweep at spec 2), less speculation once the batch is work-bound, always within
+    the fused kernels' group limit."""
+    from gladsgp_amd import _capi
+    assert mcmc.default_spec(512, 8, 11) == 3
+    assert mcmc.default_spec(512, 64, 11) < 3
+    assert mcmc.default_spec(2048, 8, 11) == 1
+    for n in (16, 512, 1024, 4096):
+        for P in (1, 8, 25, 64):
+            assert 1 <= mcmc.default_spec(n, P, 11) <= _capi.MCMC_MAX_GROUP

@@ -34,6 +34,7 @@ for step in "$@"; do
     lat) run lat 300 python -u bench.py --workload latency || exit $? ;;
     ab_cross) AB_WORKLOADS="c3 c4" run ab_cross 1000 bash tools/ab_bench_libs.sh r06_ab_cross_inner _ab/libgpfit_crossbase.so _ab/libgpfit_crossnt.so || exit $? ;;
     t_sched) run t_sched 600 $PYT tests/test_gpu_sched.py tests/test_gpu_c3.py tests/test_gpu_c4.py || exit $? ;;
+    ab_spec) run ab_spec 1000 bash -c 'for S in ${AB_SPECS:-2 3 4 4 3 2}; do echo "spec $S"; GPFIT_MCMC_SPEC=$S timeout -k 10 240 python -u bench.py --workload fit --no-cpu | tail -1 || exit 1; done' || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
