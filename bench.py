@@ -982,6 +982,14 @@ def main_c5(args):
     fy_flop = 2.0 * S * m * ny_r * P
     fy_bytes = S * m * ny_r * y.element_size() + S * m * P * 8 + P * ny_r * 8
     pr_s = ph["predict"] * 1e-3
+    c5_traffic = (None, None)
+    tf = os.path.join(ROOT, "profiles", "r06", "pmc_traffic_c5.json")
+    tj = json.load(open(tf)) if os.path.exists(tf) else {}
+    kt = tj.get("kernels", {}).get(prediction_kernel(n).split("<")[0].split(" ")[0], {})
+    if kt and (tj.get("n"), tj.get("batch"), tj.get("m")) == (n, P, m):
+        c5_traffic = (kt["bytes_per_launch"],
+                      "profiles/r06/pmc_traffic_c5.json (FETCH_SIZE x2 + WRITE_SIZE, per launch; "
+                      f"algorithmic {kt['algorithmic_bytes_per_launch']:.4g} B)")
     line = {
         "metric": "GP posterior predictions/sec fp64, C5 synthetic GlaDS ensemble (n=512 d=8, "
                   f"{ny}-node field, {P} PCs via randomized_svd, m={m}, field reconstructed)",
@@ -1007,7 +1015,8 @@ def main_c5(args):
         "roofline": {"kernel": prediction_kernel(n), "bound": "mfma",
                      "achieved": round(tr_tfs, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(tr_tfs / FP64_MFMA_PEAK_TFLOPS, 4),
-                     "traffic": None, "launches": tr_cnt,
+                     "traffic": c5_traffic[0], "traffic_source": c5_traffic[1],
+                     "launches": tr_cnt,
                      "avg_launch_ms": round(tr_ms / max(tr_cnt, 1), 4),
                      "flop_per_launch": tr_flops / max(tr_cnt, 1),
                      "work_note": "n^2 + 4n flop per prediction (the fused kernel also "

@@ -484,6 +484,9 @@ constexpr int kResCols = RES_COLS;             // test points per panel
 #ifndef RES_PROBE
 #define RES_PROBE 0
 #endif
+#ifndef RES_XCD
+#define RES_XCD 1
+#endif
 __host__ __device__ constexpr int res_waves(int RT) { return RES_WIDE ? 4 * RT : 8; }
 constexpr int kResMaxWaves = 16;
 constexpr int kResMaxPad = 512;
@@ -534,7 +537,13 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
   __shared__ double xsc[kResD * kResCols];     // sqrt(beta)-scaled test points, [dim][point]
   __shared__ double red[NW * 2 * kResCols];
   __shared__ double zs[NPAD];
+  // RES_XCD: the panels one XCD is dealt (blockIdx.x % 8 equal) are consecutive logical
+  // panels, so a problem's L^-1 is fetched into one XCD's L2 instead of all eight
+#if RES_XCD
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+#else
   const int g = blockIdx.x;
+#endif
   const int b = g / a.npanel, P = g - b * a.npanel;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -26,32 +26,41 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
         means[key.split("<")[0]][c] = sum(v) / len(v)     # trmm_pair_kernel<false> -> base name
 # the dominant kernel's HBM-side bytes per launch for bench.py's roofline.traffic: FETCH_SIZE x2
 # (gfx950 reports half the bytes of 16-B/lane streams, MI355X_MICROARCH.md HBM section) + WRITE
-t = means.get("trmm_pair_kernel", {})
+dom = "trmm_res_kernel" if WL == "c5" else "trmm_pair_kernel"
+t = means.get(dom, {})
 if t:
     if WL == "c3":
         # 6 launches per step since round 5 (the 1696-point tail runs merged with chunk 6)
         n, m, chunk, batch, launches = 4096, 100000, 16384, 1, 6
     elif WL == "c4":                     # C4: 32 GPs, n = 1024, 8192-point chunks
         n, m, chunk, batch, launches = 1024, 100000, 8192, 32, 13
-    else:                                # C5: 64 PC GPs, n = 512, 13 TRMM launches per step
+    else:                                # C5: 64 PC GPs, n = 512, 13 launches per step
         n, m, chunk, batch, launches = 512, 100000, 7936, 64, 13
     L = 8.0 * n * (n + 1) / 2 * batch    # L^-1 lower triangles
-    kt = 8.0 * n * m / launches * batch  # mean Kt chunk per launch
+    if dom == "trmm_pair_kernel":
+        alg = L + 8.0 * n * m / launches * batch          # + the launch's mean Kt chunk
+        alg_note = "L^-1 lower triangle(s) + the launch's mean Kt chunk"
+    else:                                # K* is produced in LDS: test points in, mean/var out
+        alg = L + (64.0 + 16.0 * batch) * m / launches
+        alg_note = ("L^-1 lower triangles + the launch's mean test points (64 B) and mean/var "
+                    "(16 B per prediction); K* never reaches memory.  The kernel's L^-1 loads "
+                    "are 8 B per lane (128 B per 16-lane column): the x2 correction, calibrated "
+                    "on 16-B/lane streams, is assumed to hold for them (uncalibrated width)")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of "
                      "`bench.py --steps 2 --warmup 1 --no-cpu`, MI355X (tools/pmc_traffic.sh)",
            "correction": "FETCH_SIZE x2 (gfx950 tallies 16-B/lane streams at half their bytes); "
                          "WRITE_SIZE as reported",
            "workload": WL, "m_chunk": chunk, "m": m, "n": n, "batch": batch,
-           "kernels": {"trmm_pair_kernel": {
+           "kernels": {dom: {
                "fetch_kb_raw": t.get("FETCH_SIZE"), "write_kb": t.get("WRITE_SIZE"),
                "bytes_per_launch": 1024.0 * (2 * t.get("FETCH_SIZE", 0) + t.get("WRITE_SIZE", 0)),
-               "algorithmic_bytes_per_launch": L + kt,
+               "algorithmic_bytes_per_launch": alg,
                "note": f"per-dispatch mean over the {launches} launches of a step; algorithmic = "
-                       "L^-1 lower triangle(s) + the launch's mean Kt chunk"}}}
+                       + alg_note}}}
     for k, v in means.items():
-        if k != "trmm_pair_kernel":
+        if k != dom:
             out["kernels"][k] = {"fetch_kb_raw": v.get("FETCH_SIZE"), "write_kb": v.get("WRITE_SIZE")}
     name = "pmc_traffic.json" if WL == "c3" else f"pmc_traffic_{WL}.json"
     json.dump(out, open(f"{R}/gpurun_out/{name}", "w"), indent=1)
-    print("trmm_pair_kernel bytes/launch", out["kernels"]["trmm_pair_kernel"]["bytes_per_launch"])
+    print(dom, "bytes/launch", out["kernels"][dom]["bytes_per_launch"])
 PY
