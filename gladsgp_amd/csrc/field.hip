@@ -41,6 +41,16 @@ namespace {
 #define FIELD_NT 1
 #endif
 template <int KS> constexpr int field_rows() { return KS <= 8 ? 32 : FIELD_ROWS_BIG; }
+// float32 output staged through LDS and stored 16 B per lane (a wave's row segments written by
+// one instruction each) instead of 4 B per lane from the MFMA C layout
+#ifndef FIELD_ST16
+#define FIELD_ST16 1
+#endif
+// timing probe only (no output): 1 = skip the stores
+#ifndef FIELD_PROBE
+#define FIELD_PROBE 0
+#endif
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
 #ifndef FIELD_WAVES
 #define FIELD_WAVES 4
 #endif
@@ -68,11 +78,14 @@ __global__ __launch_bounds__(kFieldThreads, FIELD_OCC) void field_kernel(const d
                                                        const double* __restrict__ mu,
                                                        const double* __restrict__ err,
                                                        void* __restrict__ Y, long long ldy,
-                                                       long long ntiles) {
+                                                       long long ntiles, bool vec16) {
   constexpr int KP = 4 * KS;                              // padded inner dimension
   constexpr int kFieldRows = field_rows<KS>(), RS = kFieldRows / 16;
   constexpr int NLD = (kFieldRows * KP + kFieldThreads - 1) / kFieldThreads;   // per thread
   __shared__ double ws[2][kFieldRows * kFieldPitch];
+  constexpr int kYP = kFieldWaveCols + 4;                 // staged row pitch (floats, 16-B rows)
+  constexpr bool ST16 = F32 && FIELD_ST16;
+  __shared__ __attribute__((aligned(16))) float ys[ST16 ? kFieldWaves * kFieldRows * kYP : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
   const long long npanels = (ncols + kFieldCols - 1) / kFieldCols;
@@ -153,6 +166,47 @@ __global__ __launch_bounds__(kFieldThreads, FIELD_OCC) void field_kernel(const d
       s_c[jt] = ok ? sd[c] : 1.0;
       m_c[jt] = ok ? mu[c] : 0.0;
     }
+    if constexpr (ST16) {
+      // the wave's kFieldRows x kFieldWaveCols float32 tile into its LDS slice (same values as
+      // the direct path), then back as 16-B row pieces: 8 lanes per 128-B row segment
+      float* yw = ys + wv * (kFieldRows * kYP);
+#pragma unroll
+      for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = 16 * rs + lk + 4 * q;
+          const long long r = r0 + rr;
+          const double e = (err && r < rows) ? err[r] : 0.0;
+#pragma unroll
+          for (int jt = 0; jt < kFieldJT; ++jt) {
+            double v = acc[rs][jt][q];
+            if (err) v = v + e;
+            if (sd) v = fma(v, s_c[jt], m_c[jt]);
+            yw[rr * kYP + 16 * jt + li] = static_cast<float>(v);
+          }
+        }
+      constexpr int kPieces = kFieldWaveCols / 4;        // 16-B pieces per row
+#pragma unroll
+      for (int h = 0; h < kFieldRows * kPieces / 64; ++h) {
+        const int idx = lane + 64 * h, rr = idx / kPieces, cc = 4 * (idx % kPieces);
+        const f32x4_t v4 = *reinterpret_cast<const f32x4_t*>(yw + rr * kYP + cc);
+        const long long r = r0 + rr;
+        const int c = c0 + cc;
+        if (r >= rows) continue;
+        float* yp = static_cast<float*>(Y) + r * ldy + c;
+#if FIELD_PROBE == 1
+        if (v4[0] == 1234.5f) *yp = v4[1];
+#else
+        if (vec16 && c + 3 < ncols) {
+          __builtin_nontemporal_store(v4, reinterpret_cast<f32x4_t*>(yp));
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (c + i < ncols) __builtin_nontemporal_store(v4[i], yp + i);
+        }
+#endif
+      }
+    } else
 #pragma unroll
     for (int rs = 0; rs < RS; ++rs)
 #pragma unroll
@@ -211,8 +265,10 @@ hipError_t launch_field(const double* W, long long ldw, int rows, int P, const d
   long long blocks = (long long)field_num_cus() *
                      (FIELD_OCC * 4 >= kFieldWaves ? FIELD_OCC * 4 / kFieldWaves : 1);
   if (blocks > npanels * ntiles) blocks = npanels * ntiles;
+  // 16-B stores need 16-B aligned rows
+  const bool vec16 = ((reinterpret_cast<uintptr_t>(Y) & 15) == 0) && (ldy % 4 == 0);
   hipLaunchKernelGGL((field_kernel<KS, F32>), dim3((unsigned)blocks), dim3(kFieldThreads), 0, stream, W,
-                     ldw, rows, P, K, ldk, ncols, sd, mu, err, Y, ldy, ntiles);
+                     ldw, rows, P, K, ldk, ncols, sd, mu, err, Y, ldy, ntiles, vec16);
   return hipGetLastError();
 }
 

@@ -12,12 +12,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # round 6 first pass (profiles/r06/r06c_field_ab.log): base (plain stores) 3.78 ms, nt 3.26,
 # 32-row tiles at one block per CU 4.52-4.75, one block per CU 5.27. Second pass
 # (r06i_field_ab.log): JT 4 / 2 blocks per CU 3.13, JT 2 / 3 per CU 3.02 (adopted), 8-wave
-# blocks 3.18-3.26, 32-row tiles at JT 2 3.13.
+# blocks 3.18-3.26, 32-row tiles at JT 2 3.13.  Late round 6: float32 output staged through LDS
+# and stored 16 B per lane (FIELD_ST16) against the 4-B stores of the MFMA C layout.
 VARIANTS = {
-    "base": [],
-    "w4j4o2": ["-DFIELD_JT=4", "-DFIELD_OCC=2"],
-    "w4j1o4": ["-DFIELD_JT=1", "-DFIELD_OCC=4"],
-    "w4j1o4r32": ["-DFIELD_JT=1", "-DFIELD_OCC=4", "-DFIELD_ROWS_BIG=32"],
+    "base": ["-DFIELD_ST16=0"],
+    "st16": [],
+    "nostore": ["-DFIELD_PROBE=1"],           # timing probe: no output written (bits differ)
 }
 
 
