@@ -65,6 +65,26 @@ def test_field_kernel_equals_generic_path(dev, P, rows, ncols):
     np.testing.assert_allclose(got, yn, rtol=1e-12, atol=1e-12 * np.abs(yn).max())
 
 
+@pytest.mark.parametrize("off", [0, 1, 2, 3])
+def test_field_f32_output_views_any_alignment(dev, off):
+    """float32 output into a column block of a wider buffer: 16-B row pieces where the rows are
+    16-B aligned (off = 0), 4-B stores otherwise; the same bits either way, nothing written
+    outside the block."""
+    from gladsgp_amd import blas
+    rng = np.random.default_rng(40 + off)
+    rows, P, ncols = 333, 64, 700
+    w = torch.as_tensor(rng.standard_normal((rows, P)), device=dev)
+    K = torch.as_tensor(rng.standard_normal((P, ncols)), device=dev)
+    sd = torch.as_tensor(rng.uniform(0.1, 3.0, ncols), device=dev)
+    mu = torch.as_tensor(rng.standard_normal(ncols), device=dev)
+    ref = blas.field(w, K, sd, mu, f32=True)
+    big = torch.full((rows, ncols + 8), 7.0, dtype=torch.float32, device=dev)
+    view = big[:, off:off + ncols]
+    blas.field(w, K, sd, mu, f32=True, out=view)
+    assert torch.equal(view, ref)
+    assert bool((big[:, :off] == 7.0).all()) and bool((big[:, off + ncols:] == 7.0).all())
+
+
 def test_get_y_beyond_field_pcs_uses_generic_path(dev):
     """P above gp_field_max_pcs() (64) reconstructs through gp_dgemm + gp_standardize: the
     kernel refuses it (-4) and get_y stays correct."""
