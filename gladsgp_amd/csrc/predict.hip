@@ -487,6 +487,11 @@ constexpr int kResCols = RES_COLS;             // test points per panel
 #ifndef RES_XCD
 #define RES_XCD 1
 #endif
+// RES_AHEAD = KA: K* produced KA chunks ahead into a 2 KA-slot LDS ring, design rows staged
+// 2 KA chunks ahead, one barrier per KA chunks
+#ifndef RES_AHEAD
+#define RES_AHEAD 3
+#endif
 __host__ __device__ constexpr int res_waves(int RT) { return RES_WIDE ? 4 * RT : 8; }
 constexpr int kResMaxWaves = 16;
 constexpr int kResMaxPad = 512;
@@ -531,11 +536,16 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
   constexpr int NPR = kResThreads / kResCols;  // K* rows one production pass covers
   constexpr int NH = (32 + NPR - 1) / NPR;     // production passes per chunk
   constexpr bool RAG = 32 % NPR != 0;          // (the last pass covers part of the chunk)
-  __shared__ __attribute__((aligned(16))) double Bs[4 * BCH];   // K* chunks c .. c + 3
+  constexpr int KA = RES_AHEAD;                // K* production distance (chunks)
+  constexpr int KSL = 2 * KA;                  // K* ring slots
+  constexpr int XA = 2 * KA;                   // design-row staging distance (<= 8: ring)
+  static_assert(XA <= 8, "design-row ring has 8 slots");
+  __shared__ __attribute__((aligned(16))) double Bs[KSL * BCH];   // K* chunks c .. c + KSL - 1
   __shared__ double tab[64];
   __shared__ double xring[9 * RING];           // design rows: chunk k in slot k & 7; scratch
   __shared__ double xsc[kResD * kResCols];     // sqrt(beta)-scaled test points, [dim][point]
-  __shared__ double red[NW * 2 * kResCols];
+  double* const red = Bs;                      // epilogue partial sums (K* ring is done)
+  static_assert(NW * 2 * kResCols <= KSL * BCH, "epilogue sums alias the K* ring");
   __shared__ double zs[NPAD];
   // RES_XCD: the panels one XCD is dealt (blockIdx.x % 8 equal) are consecutive logical
   // panels, so a problem's L^-1 is fetched into one XCD's L2 instead of all eight
@@ -576,7 +586,7 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
   // cover all 64 banks twice, conflict-free
   auto bslot = [&](int c, int h) {
     const int r = rp + NPR * h;
-    return Bs + (c & 3) * BCH + r * kResCols + (pc ^ (16 * (r & 1)));
+    return Bs + (c % KSL) * BCH + r * kResCols + (pc ^ (16 * (r & 1)));
   };
   const double sb = SLAB ? 0.0 : a.s[b];
   const bool col_ok = P * kResCols + pc < a.mv;
@@ -627,7 +637,7 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
       const int jn = (j + 1 < NJ) ? j + 1 : NJ - 1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const double* br = Bs + ((j >> 1) & 3) * BCH + ((j & 1) * 16 + 4 * q + lk) * kResCols;
+        const double* br = Bs + ((j >> 1) % KSL) * BCH + ((j & 1) * 16 + 4 * q + lk) * kResCols;
         double bv[NCT];
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) bv[ct] = br[(16 * ct + li) ^ sw];
@@ -647,15 +657,15 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
     }
   };
 
-  // ---- prologue: test points, z, design rows of chunks 0 .. 3, K* chunks 0 and 1, A(0)
+  // ---- prologue: test points, z, design rows of chunks 0 .. XA - 1, K* chunks 0 .. KA - 1, A(0)
   {
     const double zv = a.z[b * a.zld + (tid < NPAD ? tid : 0)];
     if (SLAB) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < KA; ++c)
 #pragma unroll
         for (int h = 0; h < NH; ++h)
-          if (!RAG || rp + NPR * h < 32) *bslot(c, h) = kval(c, h);
+          if (c < NCH && (!RAG || rp + NPR * h < 32)) *bslot(c, h) = kval(c, h);
     } else {
       if (tid < 64) tab[tid] = kExp2Tab[tid];
       double xs[kResCols / 32];                // test points xrow + 32 h, dimension xd
@@ -664,16 +674,16 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
         const int c_ = P * kResCols + xrow + 32 * h;
         xs[h] = a.Xs[(long long)(c_ < a.mv ? c_ : a.mv - 1) * a.ldxs + (xd < a.d ? xd : 0)];
       }
-      double x4[4];
+      double x4[XA];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) x4[c] = xval(c < NCH ? c : NCH - 1);
+      for (int c = 0; c < XA; ++c) x4[c] = xval(c < NCH ? c : NCH - 1);
       if (tid < RING) {
 #pragma unroll
         for (int h = 0; h < kResCols / 32; ++h)
           xsc[xd * kResCols + 32 * h + xrow] =
               (P * kResCols + xrow + 32 * h < a.mv && xd < a.d) ? xs[h] * bq : 0.0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) xring[c * RING + tid] = xscale(c, x4[c]);
+        for (int c = 0; c < XA; ++c) xring[c * RING + tid] = xscale(c, x4[c]);
       }
     }
     if (tid < NPAD) zs[tid] = zv;
@@ -683,17 +693,20 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
       for (int q = 0; q < 4; ++q) av[i][q] = frag(i, 0, q);
     __syncthreads();
     if (!SLAB) {
-      produce(0, 0);
-      produce(1, 1);
+#pragma unroll
+      for (int c = 0; c < KA; ++c)
+        if (c < NCH) produce(c, c);
     }
     __syncthreads();
   }
 
-  // ---- chunks: K* chunk c + 2 (produced now; SLAB: loaded now, stored after the MFMAs) into
-  // the slot chunk c - 2 used, design rows of chunk c + 4 into slot (c + 4) & 7, MFMAs of
-  // steps 2c and 2c + 1, and a barrier after every odd chunk only: whatever chunk c writes is
-  // read from chunk c + 2 on, and what it overwrites was last read at chunk c - 2, so one
-  // barrier always lies between (a barrier per chunk cost 6.5%: r06af, no-barrier probe).
+  // ---- chunks: K* chunk c + KA (produced now; SLAB: loaded now, stored after the MFMAs) into
+  // the slot chunk c - KA used, design rows of chunk c + 2 KA into slot (c + 2 KA) & 7 (read
+  // when chunk c + KA produces from them; the rows it overwrites were read at chunk c + 2 KA -
+  // 8 - KA <= c - KA), MFMAs of steps 2c and 2c + 1, and a barrier after chunks c = KA - 1
+  // mod KA only: whatever chunk c writes is read from chunk c + KA on, and what it overwrites
+  // was last read at chunk c - KA, so one barrier always lies between (a barrier per chunk cost
+  // 6.5%: r06af, no-barrier probe).
   // Tile i takes part in chunk c when T_i >= 2c (its step 2c + 1 then reads,
   // when T_i = 2c, the zero 16 x 16 block above the diagonal -- zeroed by gp_potrf_inv /
   // gp_trtri; the packed layout does not store it, so those loads select 0).  T ascends with
@@ -701,31 +714,31 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
   // each its own straight-line loop.
   auto chunk = [&](auto F, int c) {
     // (past the end: a harmless refill of the last chunk's slot with its own values)
-    const int cf = (c + 4 < NCH) ? c + 4 : NCH - 1;
+    const int cf = (c + XA < NCH) ? c + XA : NCH - 1;
     double xn = 0.0, kn[NH];
     if (SLAB) {
-      const int cn = (c + 2 < NCH) ? c + 2 : NCH - 1;
+      const int cn = (c + KA < NCH) ? c + KA : NCH - 1;
 #pragma unroll
       for (int h = 0; h < NH; ++h) kn[h] = kval(cn, h);
     } else {
       xn = xval(cf);
     }
 #if RES_PROBE != 5 && RES_PROBE != 6
-    if (!SLAB && c + 2 < NCH) produce(c + 2, (c + 2) & 7);
+    if (!SLAB && c + KA < NCH) produce(c + KA, (c + KA) & 7);
 #endif
     mstep(F, 2 * c);
     mstep(F, 2 * c + 1);
     if (SLAB) {
-      if (c + 2 < NCH) {
+      if (c + KA < NCH) {
 #pragma unroll
         for (int h = 0; h < NH; ++h)
-          if (!RAG || rp + NPR * h < 32) *bslot(c + 2, h) = kn[h];
+          if (!RAG || rp + NPR * h < 32) *bslot(c + KA, h) = kn[h];
       }
     } else {
       xring[(tid < RING ? (cf & 7) : 8) * RING + (tid & (RING - 1))] = xscale(cf, xn);
     }
 #if RES_PROBE != 3 && RES_PROBE != 6
-    if (c & 1) __syncthreads();
+    if (c % KA == KA - 1) __syncthreads();
 #endif
   };
   int c = 0;
@@ -739,6 +752,7 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
 
   // ---- epilogue: per column sum V z and sum V^2 over the wave's rows (C layout: lane l, reg
   // r holds row 16 T + (l >> 4) + 4 r, column l & 15), then over the 8 waves in a fixed order
+  double smv[NCT], svv[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {
     double sm = 0.0, sv = 0.0;
@@ -754,9 +768,17 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
     sv += __shfl_xor(sv, 16, 64);
     sm += __shfl_xor(sm, 32, 64);
     sv += __shfl_xor(sv, 32, 64);
-    if (lk == 0) {
-      red[(w * 2 + 0) * kResCols + ct * 16 + li] = sm;
-      red[(w * 2 + 1) * kResCols + ct * 16 + li] = sv;
+    smv[ct] = sm;
+    svv[ct] = sv;
+  }
+  // red overwrites the K* ring: every wave has finished its last chunk's reads (the last chunk
+  // ends with a barrier only when NCH - 1 = KA - 1 mod KA)
+  if ((NCH - 1) % KA != KA - 1) __syncthreads();
+  if (lk == 0) {
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      red[(w * 2 + 0) * kResCols + ct * 16 + li] = smv[ct];
+      red[(w * 2 + 1) * kResCols + ct * 16 + li] = svv[ct];
     }
   }
   __syncthreads();
