@@ -438,16 +438,17 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
 // trip through HBM (the cross-covariance chunk written, then read by every row-tile pair).
 // Here a panel is kResCols = 64 test points of one problem, and one block computes ALL npad
 // rows of V = L^-1 K*^T for it:
-//   * K*'s panel passes through a four-chunk LDS ring (64 KB), produced 32 rows (a chunk) at
-//     a time, two chunks ahead, by the block's own threads: s exp(-sum (sqrt(beta)(x_k -
-//     x*_j))^2) with cross_kp_kernel's exact arithmetic (the same Kt values bit for bit), one
-//     exp per element -- no cross-covariance kernel, no Kt slab in HBM;
+//   * K*'s panel passes through a 2 RES_AHEAD-chunk LDS ring (6 chunks, 96 KB), produced 32
+//     rows (a chunk) at a time, RES_AHEAD chunks ahead, by the block's own threads:
+//     s exp(-sum (sqrt(beta)(x_k - x*_j))^2) with cross_kp_kernel's exact arithmetic (the same
+//     Kt values bit for bit), one exp per element -- no cross-covariance kernel, no Kt slab in
+//     HBM;
 //   * L^-1 (1 MB lower triangle per problem at n = 512, L2-resident: panels are problem-major,
 //     so the chip works through one problem's panels at a time) streams straight into
 //     registers as MFMA A fragments by buffer loads (wave-uniform offset + four per-lane
 //     offsets: no vector address arithmetic), one 16-k step ahead;
 //   * 8 waves, wave w owning the 16-row tiles {w, 15 - w, 16 + w, 31 - w} (the first RT of
-//     them: equal sums of (T + 1), i.e. equal MFMA work), both 16-column MFMA tiles;
+//     them: equal sums of (T + 1), i.e. equal MFMA work), all four 16-column MFMA tiles;
 //   * tile T meets L^-1 at k-steps j <= T; activity is resolved per chunk (steps 2c, 2c + 1:
 //     tile i takes part when T_i >= 2c, its step 2c + 1 then reading, when T_i = 2c, the zero
 //     16 x 16 block above the diagonal -- zeroed by gp_potrf_inv / gp_trtri; the packed layout
@@ -457,14 +458,15 @@ __global__ __launch_bounds__(256, 2) void trmm_pair_kernel(const TrmmArgs a) {
 //   * one block per panel (a persistent form that streamed a block's panels as one chunk
 //     sequence, loading the next panel's inputs under the last chunks, measured no faster:
 //     profiles/r06/r06ah_ab_res_persistent.log);
-//   * one barrier per two chunks, one more per panel for the epilogue, which reduces sum V z
-//     and sum V^2 over the panel's rows and writes mean / var directly (no slab, no finalize).
+//   * one barrier per RES_AHEAD chunks, one more per panel for the epilogue, which reduces
+//     sum V z and sum V^2 over the panel's rows and writes mean / var directly (no slab, no
+//     finalize).
 // Every global load is issued unconditionally (at a clamped in-bounds address when its value
 // is not needed): the same number of loads on every path keeps the compiler's vmcnt waits
 // counted, so prefetches stay in flight across the MFMAs.
 // SLAB: K* read from a materialised cross-covariance chunk instead (gp_predict_solve after
-// gp_predict_cross, and d > 8), two chunks ahead through registers -- the same Kt values, so
-// every entry point gives the same bits at npad <= 512.
+// gp_predict_cross, and d > 8), RES_AHEAD chunks ahead through registers -- the same Kt
+// values, so every entry point gives the same bits at npad <= 512.
 // Sums run k ascending in every tile (the pair kernel runs some tiles diagonal-block first), so
 // results equal the pair path to rounding, not bit for bit; they do not depend on the chunking.
 #ifndef RES_COLS
