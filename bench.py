@@ -503,7 +503,7 @@ def main():
     tr_tfs = tr_flops / (tr_ms * 1e-3) / 1e12
     traffic, traffic_src = None, None
     chunk = args.m_chunk or 16384   # the library's default test-point chunk for one GP
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         tf = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         tj = json.load(open(tf)) if os.path.exists(tf) else {}
         if tj and n == 4096 and chunk == tj.get("m_chunk") and ml == tj.get("m", 100000):
@@ -675,7 +675,7 @@ def main_c4(args):
     value = P * m * K / elapsed
     tr_flops = float(bl) * m * K * (n * n + 4 * n)
     traffic, traffic_src = None, None
-    for rnd in ("r05", "r04", "r03"):
+    for rnd in ("r06", "r05", "r04", "r03"):
         tf = os.path.join(ROOT, "profiles", rnd, "pmc_traffic_c4.json")
         if not (os.path.exists(tf) and ctx.world == 1):
             continue
