@@ -540,8 +540,14 @@ __global__ __launch_bounds__(64 * res_waves(RT), RES_WIDE ? RT : RES_OCC) void t
   constexpr bool RAG = 32 % NPR != 0;          // (the last pass covers part of the chunk)
   constexpr int KA = RES_AHEAD;                // K* production distance (chunks)
   constexpr int KSL = 2 * KA;                  // K* ring slots
-  constexpr int XA = 2 * KA;                   // design-row staging distance (<= 8: ring)
-  static_assert(XA <= 8, "design-row ring has 8 slots");
+  // design-row staging distance: rows written at chunk c are read when chunk c + XA - KA
+  // produces from them (needs XA >= 2 KA) and overwrite rows read at c + XA - 8 - KA (XA <= 8)
+#ifdef RES_XA
+  constexpr int XA = RES_XA;
+#else
+  constexpr int XA = 2 * KA;
+#endif
+  static_assert(XA >= 2 * KA && XA <= 8, "design-row ring has 8 slots");
   __shared__ __attribute__((aligned(16))) double Bs[KSL * BCH];   // K* chunks c .. c + KSL - 1
   __shared__ double tab[64];
   __shared__ double xring[9 * RING];           // design rows: chunk k in slot k & 7; scratch
